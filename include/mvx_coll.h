@@ -1,0 +1,171 @@
+/*
+ * mvx_coll.h -- libmvx.so, the C host library of the MI355X reduction path.
+ *
+ * Drop-in surface (same names, argument meaning and return codes as the
+ * reference):
+ *   MPI_Reduce / MPI_Allreduce / MPI_Reduce_scatter   include/mpi.h:400-404,
+ *     bodies src/coll/reduce.c:62-96, allreduce.c:57-92, red_scat.c:60-90
+ *   MPI_Op_create / MPI_Op_free                        src/coll/opcreate.c:62-76,
+ *                                                      opfree.c:51-82
+ *   MPIR_MAXF ... MPIR_MINLOC (MPI_User_function)      include/mpiimpl.h:201-212
+ *   struct mvx_collops {Reduce, Allreduce, Reduce_scatter}
+ *                                                      include/mpicoll.h:41-49
+ * plus PMPI_ twins (include/mpi.h:589-593).
+ *
+ * Buffers may be device memory (the fast path: RCCL over xGMI moves shards,
+ * libmvx_hip.so kernels do the arithmetic in the reference's combine order)
+ * or host memory (staged through HBM; see DESIGN.md for the PCIe-inclusive
+ * rate).  The blocking MPI_* calls return with the result in recvbuf; the
+ * mvx_*_async variants are stream-ordered on the given HIP stream.
+ */
+#ifndef MVX_COLL_H
+#define MVX_COLL_H
+
+#include <stddef.h>
+#include "mvx_mpi.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- communicators ----------------------------------------------------- */
+#define MVX_UNIQUE_ID_BYTES 128
+
+/* rank 0 creates the id, every rank passes the same bytes to mvx_comm_init */
+int mvx_get_unique_id(void *id_out);
+/* one process per GPU: collective over `size` processes (RCCL over xGMI);
+ * the first communicator created becomes MPI_COMM_WORLD. */
+int mvx_comm_init(MPI_Comm *comm, int rank, int size, int device,
+                  const void *unique_id);
+/* `size` virtual ranks in this process on one device (loopback transport,
+ * device-to-device copies); use the *_multi entry points with it. */
+int mvx_comm_init_local(MPI_Comm *comm, int size, int device);
+int mvx_comm_free(MPI_Comm *comm);
+int MPI_Comm_size(MPI_Comm comm, int *size);
+int MPI_Comm_rank(MPI_Comm comm, int *rank);
+/* stream the blocking calls run on (default: the null stream) */
+int mvx_comm_set_stream(MPI_Comm comm, void *hip_stream);
+/* pre-size the staging pool so no allocation happens inside a call */
+int mvx_comm_reserve(MPI_Comm comm, size_t bytes);
+
+/* ---- MPI API (blocking) ------------------------------------------------ */
+int MPI_Reduce(void *sendbuf, void *recvbuf, int count, MPI_Datatype datatype,
+               MPI_Op op, int root, MPI_Comm comm);
+int MPI_Allreduce(void *sendbuf, void *recvbuf, int count,
+                  MPI_Datatype datatype, MPI_Op op, MPI_Comm comm);
+int MPI_Reduce_scatter(void *sendbuf, void *recvbuf, int *recvcnts,
+                       MPI_Datatype datatype, MPI_Op op, MPI_Comm comm);
+int MPI_Op_create(MPI_User_function *function, int commute, MPI_Op *op);
+int MPI_Op_free(MPI_Op *op);
+int MPI_Error_class(int errorcode, int *errorclass);
+
+int PMPI_Reduce(void *, void *, int, MPI_Datatype, MPI_Op, int, MPI_Comm);
+int PMPI_Allreduce(void *, void *, int, MPI_Datatype, MPI_Op, MPI_Comm);
+int PMPI_Reduce_scatter(void *, void *, int *, MPI_Datatype, MPI_Op, MPI_Comm);
+int PMPI_Op_create(MPI_User_function *, int, MPI_Op *);
+int PMPI_Op_free(MPI_Op *);
+
+/* ---- stream-ordered variants (device buffers only) --------------------- */
+int mvx_reduce_async(const void *sendbuf, void *recvbuf, int count,
+                     MPI_Datatype datatype, MPI_Op op, int root, MPI_Comm comm,
+                     void *hip_stream);
+int mvx_allreduce_async(const void *sendbuf, void *recvbuf, int count,
+                        MPI_Datatype datatype, MPI_Op op, MPI_Comm comm,
+                        void *hip_stream);
+int mvx_reduce_scatter_async(const void *sendbuf, void *recvbuf,
+                             const int *recvcnts, MPI_Datatype datatype,
+                             MPI_Op op, MPI_Comm comm, void *hip_stream);
+
+/* ---- virtual communicators: all ranks' buffers in this process ---------- */
+/* rc[r] receives rank r's return code; the function returns MPI_SUCCESS or
+ * the first argument error. */
+int mvx_reduce_multi(void *const *sendbufs, void *const *recvbufs, int count,
+                     MPI_Datatype datatype, MPI_Op op, int root, MPI_Comm comm,
+                     int *rc, void *hip_stream);
+int mvx_allreduce_multi(void *const *sendbufs, void *const *recvbufs,
+                        int count, MPI_Datatype datatype, MPI_Op op,
+                        MPI_Comm comm, int *rc, void *hip_stream);
+int mvx_reduce_scatter_multi(void *const *sendbufs, void *const *recvbufs,
+                             const int *recvcnts, MPI_Datatype datatype,
+                             MPI_Op op, MPI_Comm comm, int *rc,
+                             void *hip_stream);
+
+/* ---- collective function table (mpicoll.h:41-49 members, by handle) ---- */
+typedef struct mvx_collops {
+    int (*Reduce)(void *, void *, int, MPI_Datatype, MPI_Op, int, MPI_Comm);
+    int (*Allreduce)(void *, void *, int, MPI_Datatype, MPI_Op, MPI_Comm);
+    int (*Reduce_scatter)(void *, void *, int *, MPI_Datatype, MPI_Op,
+                          MPI_Comm);
+} mvx_collops;
+extern const mvx_collops MVX_device_collops;
+
+/* ---- predefined ops as MPI_User_functions (global_ops.c) ---------------
+ * invec / inoutvec must be device-accessible; the call completes before it
+ * returns.  An undefined (op, type) pair leaves the data alone and sets
+ * mvx_op_errno() to 329, as MPIR_Op_errno (global_ops.c:41). */
+void MPIR_MAXF(void *, void *, int *, MPI_Datatype *);
+void MPIR_MINF(void *, void *, int *, MPI_Datatype *);
+void MPIR_SUM(void *, void *, int *, MPI_Datatype *);
+void MPIR_PROD(void *, void *, int *, MPI_Datatype *);
+void MPIR_LAND(void *, void *, int *, MPI_Datatype *);
+void MPIR_BAND(void *, void *, int *, MPI_Datatype *);
+void MPIR_LOR(void *, void *, int *, MPI_Datatype *);
+void MPIR_BOR(void *, void *, int *, MPI_Datatype *);
+void MPIR_LXOR(void *, void *, int *, MPI_Datatype *);
+void MPIR_BXOR(void *, void *, int *, MPI_Datatype *);
+void MPIR_MAXLOC(void *, void *, int *, MPI_Datatype *);
+void MPIR_MINLOC(void *, void *, int *, MPI_Datatype *);
+int mvx_op_errno(void);
+
+/* ---- plans (host logic, no device needed; exported for tests) ----------- */
+#define MVX_MAXP 64
+#define MVX_MAXK 64
+
+#define MVX_COLL_ALLREDUCE      1
+#define MVX_COLL_REDUCE         2
+#define MVX_COLL_REDUCE_SCATTER 3
+
+#define MVX_ALG_NONE          0
+#define MVX_ALG_RECDBL        1
+#define MVX_ALG_RABENSEIFNER  2
+#define MVX_ALG_BINOMIAL      3
+#define MVX_ALG_RS_HALVING    4
+#define MVX_ALG_RS_PAIRWISE   5
+
+typedef struct { long off, cnt; } mvx_range;   /* in elements */
+
+/* What rank `rank` does for one collective call.  Phase A: send ranges of
+ * its sendbuf, receive other ranks' sendbuf ranges into staging slot s.
+ * Phase B: one k-leaf combine (leaf q = rank leaf[q]'s data, folded with
+ * rank leaf_fold[q]'s data when >= 0) over elements [c_src_off, +c_cnt) of
+ * the source vectors, written to recvbuf + c_dst_off (c_dst_tmp = 0) or to
+ * a temporary (1).  Phase C: send the combine output to the ranks in
+ * b_send (destination recvbuf coordinates), receive b_recv ranges into
+ * recvbuf. */
+typedef struct mvx_plan {
+    int coll, alg, p, rank, root, op, dtype, esize;
+    int symmetric;      /* result independent of operand roles */
+    int calls_uop;      /* the reference calls (*uop) on this rank */
+    long count;         /* vector elements (Reduce_scatter: total) */
+    mvx_range a_send[MVX_MAXP];
+    mvx_range a_recv[MVX_MAXP];
+    int has_combine, k, shape, c_dst_tmp;
+    int leaf[MVX_MAXK];
+    int leaf_fold[MVX_MAXK];
+    long c_src_off, c_cnt, c_dst_off;
+    mvx_range b_send[MVX_MAXP];
+    mvx_range b_recv[MVX_MAXP];
+} mvx_plan;
+
+/* Builds rank `rank`'s plan; returns 0 or an MPI error class. */
+int mvx_plan_build(mvx_plan *plan, int coll, int p, int rank, long count,
+                   const int *recvcnts, int dtype, int op, int root);
+/* The reference's algorithm for (coll, p, total elements, dtype). */
+int mvx_plan_algorithm(int coll, int p, long total_count, int dtype);
+/* Datatype facts: extent and MPI_Type_size; returns 0 or MPI_ERR_TYPE. */
+int mvx_dtype_info(int dtype, int *extent, int *type_size);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MVX_COLL_H */

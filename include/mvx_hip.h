@@ -1,0 +1,78 @@
+/*
+ * mvx_hip.h -- C-ABI of libmvx_hip.so, the thin device layer of the
+ * reduction path (hand-written HIP for gfx950).
+ *
+ * Every entry point takes plain device pointers and element counts, is
+ * stream-ordered (nothing synchronises unless stated), allocates nothing,
+ * takes no ownership, and returns an MPI error code instead of setting a
+ * global errno (the reference's MPIR_Op_errno, coll.h:61-68, is replaced by
+ * the return value).
+ *
+ * Reference interfaces replaced:
+ *   mvx_op_apply     the predefined op kernels MPIR_MAXF ... MPIR_MINLOC,
+ *                    src/coll/global_ops.c:56-1745, called through
+ *                    MPI_User_function (include/mpi.h:206) as
+ *                    (*uop)(invec, inoutvec, &len, &type), e.g.
+ *                    src/coll/intra_fns_new.c:5697.
+ *   mvx_op_combine   a whole chain of (*uop) calls of one collective in one
+ *                    HBM pass: the Rabenseifner / recursive-doubling tree
+ *                    (intra_fns_new.c:5592-5710, 4697-4751), the binomial
+ *                    tree (4907-4954), the recursive-halving tree
+ *                    (6341-6407) and the pairwise chain (6473-6500), with the
+ *                    operand order fixed by the caller's leaf permutation.
+ *   mvx_op_supported the (op, type) validity switch of each op function
+ *                    (e.g. global_ops.c:158-161).
+ */
+#ifndef MVX_HIP_H
+#define MVX_HIP_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Combine shapes over leaves y[0..k-1] (a = left operand = inout role):
+ *  MVX_SHAPE_TREE : S(q,0)=y[q]; S(q,l)=op(S(q,l-1), S(q+2^(l-1),l-1)) when
+ *                   q+2^(l-1) < k, else S(q,l-1); result S(0, ceil(log2 k)).
+ *                   For k = 2^L this is ((y0 y1)(y2 y3))...; for other k it is
+ *                   the binomial tree truncated at k.
+ *  MVX_SHAPE_CHAIN: (((y0 y1) y2) ... y(k-1)). */
+#define MVX_SHAPE_TREE  0
+#define MVX_SHAPE_CHAIN 1
+
+/* Largest k one combine launch takes. */
+#define MVX_COMBINE_KMAX 8
+
+/* 1 if a device kernel exists for (op, dtype); 0 otherwise. */
+int mvx_op_supported(int op, int dtype);
+
+/* Bytes per element (the datatype extent) on the device path, or 0. */
+int mvx_dtype_extent(int dtype);
+
+/* inout[i] = in[i] op inout[i], i < n.  Returns MPI_SUCCESS, 329 for an
+ * undefined (op, type) pair (as MPIR_ERR_OP_NOT_DEFINED), MPI_ERR_OP for an
+ * unknown op handle, MPI_ERR_TYPE for a datatype with no device
+ * representation (MPI_LONG_DOUBLE, MPI_LONG_DOUBLE_INT). */
+int mvx_op_apply(int op, int dtype, const void *in, void *inout, size_t n,
+                 void *hip_stream);
+
+/* dst[i] = shape-combine over leaves; leaf q = srcs[q][i] if fold == NULL or
+ * fold[q] == NULL, else op(srcs[q][i], fold[q][i]) (srcs[q] is the inout
+ * role).  srcs / fold are HOST arrays of k device pointers; 1 <= k <=
+ * MVX_COMBINE_KMAX.  dst may alias srcs[0] (only).  Same return codes as
+ * mvx_op_apply, plus MPI_ERR_ARG for a bad k / shape. */
+int mvx_op_combine(int op, int dtype, const void *const *srcs,
+                   const void *const *fold, int k, int shape, void *dst,
+                   size_t n, void *hip_stream);
+
+/* Launch geometry knobs (0 = default), for the tuning sweep in bench.py. */
+void mvx_hip_set_launch(int block_cap, int unroll_variant);
+
+/* Name of the last kernel launched (for profile attribution in bench.py). */
+const char *mvx_hip_last_kernel(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MVX_HIP_H */

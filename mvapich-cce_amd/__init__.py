@@ -1,0 +1,174 @@
+"""mvapich-cce_amd -- MI355X-native MPI reduction path (Python host mirror).
+
+The product is two in-tree shared libraries built from ``csrc/``:
+
+* ``libmvx_hip.so`` -- hand-written HIP kernels for gfx950 behind the C-ABI of
+  ``include/mvx_hip.h`` (``mvx_op_apply``, ``mvx_op_combine``, ...);
+* ``libmvx.so`` -- the C host library of ``include/mvx_coll.h``:
+  ``MPI_Reduce`` / ``MPI_Allreduce`` / ``MPI_Reduce_scatter`` /
+  ``MPI_Op_create`` / ``MPI_Op_free`` / ``MPIR_SUM`` ... with the reference's
+  handles and error codes, plans in the reference's combine order, RCCL for
+  the data movement.
+
+This module binds them with ctypes and mirrors the reference's C interface
+(same function names, argument meaning and return codes) so tests read like
+the reference's ``examples/test/coll/*.c``.  It never computes anything
+itself: if the libraries are missing it raises.
+"""
+import ctypes
+import os
+
+from . import consts as C  # noqa: F401  (re-exported handles)
+from .consts import *  # noqa: F401,F403
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_HIP = os.path.join(HERE, "libmvx_hip.so")
+LIB_COLL = os.path.join(HERE, "libmvx.so")
+
+_hip = None
+_coll = None
+
+
+class NativeMissing(RuntimeError):
+    pass
+
+
+def build(verbose=False):
+    """Compile both libraries in-tree (hipcc for gfx950, gcc for the host)."""
+    import subprocess
+    jobs = os.environ.get("MAX_JOBS", "4")
+    cmd = ["make", "-C", os.path.join(HERE, "csrc"), "-j", jobs]
+    if not verbose:
+        cmd.insert(1, "-s")
+    subprocess.check_call(cmd)
+
+
+class Range(ctypes.Structure):
+    _fields_ = [("off", ctypes.c_long), ("cnt", ctypes.c_long)]
+
+
+MAXP = 64
+MAXK = 64
+
+
+class Plan(ctypes.Structure):
+    """Mirror of ``mvx_plan`` (include/mvx_coll.h)."""
+    _fields_ = [
+        ("coll", ctypes.c_int), ("alg", ctypes.c_int), ("p", ctypes.c_int), ("rank", ctypes.c_int),
+        ("root", ctypes.c_int), ("op", ctypes.c_int), ("dtype", ctypes.c_int), ("esize", ctypes.c_int),
+        ("symmetric", ctypes.c_int), ("calls_uop", ctypes.c_int), ("count", ctypes.c_long),
+        ("a_send", Range * MAXP), ("a_recv", Range * MAXP),
+        ("has_combine", ctypes.c_int), ("k", ctypes.c_int), ("shape", ctypes.c_int), ("c_dst_tmp", ctypes.c_int),
+        ("leaf", ctypes.c_int * MAXK), ("leaf_fold", ctypes.c_int * MAXK),
+        ("c_src_off", ctypes.c_long), ("c_cnt", ctypes.c_long), ("c_dst_off", ctypes.c_long),
+        ("b_send", Range * MAXP), ("b_recv", Range * MAXP),
+    ]
+
+
+def _load():
+    global _hip, _coll
+    if _coll is not None:
+        return
+    if not (os.path.exists(LIB_HIP) and os.path.exists(LIB_COLL)):
+        raise NativeMissing("libmvx_hip.so / libmvx.so not built: run __graft_entry__.build() "
+                            "(there is no non-native fallback)")
+    # If torch is in use it must own the HIP runtime: load it first so the
+    # libamdhip64.so.7 / librccl.so.1 SONAMEs resolve to its copies.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+    _hip = ctypes.CDLL(LIB_HIP, mode=ctypes.RTLD_GLOBAL)
+    _coll = ctypes.CDLL(LIB_COLL, mode=ctypes.RTLD_GLOBAL)
+    vp, i, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
+    pi = ctypes.POINTER(ctypes.c_int)
+    pvp = ctypes.POINTER(ctypes.c_void_p)
+    _hip.mvx_op_supported.argtypes = [i, i]
+    _hip.mvx_dtype_extent.argtypes = [i]
+    _hip.mvx_op_apply.argtypes = [i, i, vp, vp, sz, vp]
+    _hip.mvx_op_combine.argtypes = [i, i, pvp, pvp, i, i, vp, sz, vp]
+    _hip.mvx_hip_set_launch.argtypes = [i, i]
+    _hip.mvx_hip_set_launch.restype = None
+    _hip.mvx_hip_last_kernel.restype = ctypes.c_char_p
+    c = _coll
+    c.mvx_get_unique_id.argtypes = [vp]
+    c.mvx_comm_init.argtypes = [pi, i, i, i, vp]
+    c.mvx_comm_init_local.argtypes = [pi, i, i]
+    c.mvx_comm_free.argtypes = [pi]
+    c.mvx_comm_set_stream.argtypes = [i, vp]
+    c.mvx_comm_reserve.argtypes = [i, sz]
+    c.MPI_Comm_size.argtypes = [i, pi]
+    c.MPI_Comm_rank.argtypes = [i, pi]
+    for name in ("MPI_Allreduce", "PMPI_Allreduce"):
+        getattr(c, name).argtypes = [vp, vp, i, i, i, i]
+    for name in ("MPI_Reduce", "PMPI_Reduce"):
+        getattr(c, name).argtypes = [vp, vp, i, i, i, i, i]
+    for name in ("MPI_Reduce_scatter", "PMPI_Reduce_scatter"):
+        getattr(c, name).argtypes = [vp, vp, pi, i, i, i]
+    c.MPI_Op_create.argtypes = [vp, i, pi]
+    c.MPI_Op_free.argtypes = [pi]
+    c.MPI_Error_class.argtypes = [i, pi]
+    c.mvx_allreduce_async.argtypes = [vp, vp, i, i, i, i, vp]
+    c.mvx_reduce_async.argtypes = [vp, vp, i, i, i, i, i, vp]
+    c.mvx_reduce_scatter_async.argtypes = [vp, vp, pi, i, i, i, vp]
+    c.mvx_allreduce_multi.argtypes = [pvp, pvp, i, i, i, i, pi, vp]
+    c.mvx_reduce_multi.argtypes = [pvp, pvp, i, i, i, i, i, pi, vp]
+    c.mvx_reduce_scatter_multi.argtypes = [pvp, pvp, pi, i, i, i, pi, vp]
+    c.mvx_plan_build.argtypes = [ctypes.POINTER(Plan), i, i, i, ctypes.c_long, pi, i, i, i]
+    c.mvx_plan_algorithm.argtypes = [i, i, ctypes.c_long, i]
+    c.mvx_dtype_info.argtypes = [i, pi, pi]
+    for name in ("MPIR_MAXF", "MPIR_MINF", "MPIR_SUM", "MPIR_PROD", "MPIR_LAND", "MPIR_BAND", "MPIR_LOR",
+                 "MPIR_BOR", "MPIR_LXOR", "MPIR_BXOR", "MPIR_MAXLOC", "MPIR_MINLOC"):
+        fn = getattr(c, name)
+        fn.argtypes = [vp, vp, pi, pi]
+        fn.restype = None
+
+
+def hip():
+    _load()
+    return _hip
+
+
+def coll():
+    _load()
+    return _coll
+
+
+def loaded_paths():
+    """Absolute paths of the native libraries this process has loaded."""
+    _load()
+    return [LIB_HIP, LIB_COLL]
+
+
+# ---------------------------------------------------------------- plans ----
+
+def plan(coll_kind, p, rank, count, dtype, op, root=0, recvcnts=None):
+    P = Plan()
+    rc_arr = None
+    if recvcnts is not None:
+        rc_arr = (ctypes.c_int * p)(*recvcnts)
+    rc = coll().mvx_plan_build(ctypes.byref(P), coll_kind, p, rank, count, rc_arr, dtype, op, root)
+    if rc:
+        raise ValueError("mvx_plan_build rc=%d" % rc)
+    return P
+
+
+def algorithm(coll_kind, p, total, dtype):
+    return coll().mvx_plan_algorithm(coll_kind, p, total, dtype)
+
+
+def dtype_info(dtype):
+    e, s = ctypes.c_int(), ctypes.c_int()
+    rc = coll().mvx_dtype_info(dtype, ctypes.byref(e), ctypes.byref(s))
+    if rc:
+        raise ValueError("unregistered datatype %d" % dtype)
+    return e.value, s.value
+
+
+def error_class(code):
+    c = ctypes.c_int()
+    coll().MPI_Error_class(code, ctypes.byref(c))
+    return c.value
+
+
+from .api import *  # noqa: E402,F401,F403

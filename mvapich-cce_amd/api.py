@@ -1,0 +1,201 @@
+"""Reference-shaped entry points over libmvx.so / libmvx_hip.so.
+
+Buffers may be torch tensors (device or host), numpy arrays (host) or raw
+integer addresses.  Return values are the C library's MPI error codes,
+exactly as the reference's MPI_* functions return them.
+"""
+import ctypes
+
+from . import coll, hip
+from .consts import COLL_ALLREDUCE, COLL_REDUCE, COLL_REDUCE_SCATTER  # noqa: F401
+
+__all__ = [
+    "addr", "stream_handle", "op_apply", "op_combine", "Comm",
+    "MPI_Allreduce", "MPI_Reduce", "MPI_Reduce_scatter", "MPI_Op_create", "MPI_Op_free",
+    "MPIR_call", "op_errno", "last_kernel", "set_launch",
+]
+
+
+def addr(buf):
+    """Address of a tensor / ndarray / int (None -> 0)."""
+    if buf is None:
+        return 0
+    if isinstance(buf, int):
+        return buf
+    if hasattr(buf, "data_ptr"):
+        return buf.data_ptr()
+    if hasattr(buf, "ctypes"):
+        return buf.ctypes.data
+    raise TypeError("cannot take the address of %r" % type(buf))
+
+
+def stream_handle(stream=None):
+    """hipStream_t of a torch stream (default: torch's current stream)."""
+    if isinstance(stream, int):
+        return stream
+    import torch
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return s.cuda_stream
+
+
+def _pp(ptrs):
+    arr = (ctypes.c_void_p * len(ptrs))()
+    for i, p in enumerate(ptrs):
+        arr[i] = addr(p) or None
+    return arr
+
+
+def op_apply(op, dtype, invec, inoutvec, n, stream=None):
+    """inoutvec = invec op inoutvec on the device (stream-ordered)."""
+    return hip().mvx_op_apply(op, dtype, addr(invec), addr(inoutvec), n, stream_handle(stream))
+
+
+def op_combine(op, dtype, srcs, dst, n, shape=0, folds=None, stream=None):
+    """dst = shape-combine of leaves srcs (each optionally folded)."""
+    k = len(srcs)
+    fo = _pp(folds) if folds is not None else None
+    return hip().mvx_op_combine(op, dtype, _pp(srcs), fo, k, shape, addr(dst), n, stream_handle(stream))
+
+
+def set_launch(block_cap=0, unroll=0):
+    hip().mvx_hip_set_launch(block_cap, unroll)
+
+
+def last_kernel():
+    return hip().mvx_hip_last_kernel().decode()
+
+
+# ------------------------------------------------------------- communicators
+
+class Comm:
+    """An MPI_Comm handle of libmvx.so."""
+
+    def __init__(self, handle, rank, size, local):
+        self.handle, self.rank, self.size, self.local = handle, rank, size, local
+
+    @classmethod
+    def from_torch_distributed(cls, device=None):
+        """One rank per GPU: RCCL communicator bootstrapped over the already
+        initialised torch.distributed process group (any backend)."""
+        import torch
+        import torch.distributed as dist
+        rank, size = dist.get_rank(), dist.get_world_size()
+        if device is None:
+            device = torch.cuda.current_device()
+        uid = ctypes.create_string_buffer(128)
+        if rank == 0:
+            rc = coll().mvx_get_unique_id(uid)
+            if rc:
+                raise RuntimeError("mvx_get_unique_id rc=%d" % rc)
+        box = [bytes(uid.raw) if rank == 0 else None]
+        dist.broadcast_object_list(box, src=0)
+        uid = ctypes.create_string_buffer(box[0], 128)
+        h = ctypes.c_int()
+        rc = coll().mvx_comm_init(ctypes.byref(h), rank, size, device, uid)
+        if rc:
+            raise RuntimeError("mvx_comm_init rc=%d" % rc)
+        return cls(h.value, rank, size, False)
+
+    @classmethod
+    def local_ranks(cls, size, device=0):
+        """`size` virtual ranks on one device (use the *_multi methods)."""
+        h = ctypes.c_int()
+        rc = coll().mvx_comm_init_local(ctypes.byref(h), size, device)
+        if rc:
+            raise RuntimeError("mvx_comm_init_local rc=%d" % rc)
+        return cls(h.value, 0, size, True)
+
+    def free(self):
+        h = ctypes.c_int(self.handle)
+        coll().mvx_comm_free(ctypes.byref(h))
+
+    def set_stream(self, stream=None):
+        return coll().mvx_comm_set_stream(self.handle, stream_handle(stream))
+
+    def reserve(self, nbytes):
+        return coll().mvx_comm_reserve(self.handle, nbytes)
+
+    # stream-ordered (device buffers)
+    def allreduce_async(self, sendbuf, recvbuf, count, dtype, op, stream=None):
+        return coll().mvx_allreduce_async(addr(sendbuf), addr(recvbuf), count, dtype, op, self.handle,
+                                          stream_handle(stream))
+
+    def reduce_async(self, sendbuf, recvbuf, count, dtype, op, root, stream=None):
+        return coll().mvx_reduce_async(addr(sendbuf), addr(recvbuf), count, dtype, op, root, self.handle,
+                                       stream_handle(stream))
+
+    def reduce_scatter_async(self, sendbuf, recvbuf, recvcnts, dtype, op, stream=None):
+        cn = (ctypes.c_int * len(recvcnts))(*recvcnts)
+        return coll().mvx_reduce_scatter_async(addr(sendbuf), addr(recvbuf), cn, dtype, op, self.handle,
+                                               stream_handle(stream))
+
+    # virtual communicators: all ranks' buffers at once, per-rank codes back
+    def allreduce_multi(self, sendbufs, recvbufs, count, dtype, op, stream=None):
+        rc = (ctypes.c_int * self.size)()
+        r = coll().mvx_allreduce_multi(_pp(sendbufs), _pp(recvbufs), count, dtype, op, self.handle, rc,
+                                       stream_handle(stream))
+        return r, list(rc)
+
+    def reduce_multi(self, sendbufs, recvbufs, count, dtype, op, root, stream=None):
+        rc = (ctypes.c_int * self.size)()
+        r = coll().mvx_reduce_multi(_pp(sendbufs), _pp(recvbufs), count, dtype, op, root, self.handle, rc,
+                                    stream_handle(stream))
+        return r, list(rc)
+
+    def reduce_scatter_multi(self, sendbufs, recvbufs, recvcnts, dtype, op, stream=None):
+        rc = (ctypes.c_int * self.size)()
+        cn = (ctypes.c_int * self.size)(*recvcnts)
+        r = coll().mvx_reduce_scatter_multi(_pp(sendbufs), _pp(recvbufs), cn, dtype, op, self.handle, rc,
+                                            stream_handle(stream))
+        return r, list(rc)
+
+
+def _comm_handle(comm):
+    return comm.handle if isinstance(comm, Comm) else comm
+
+
+# -------------------------------------------------------- MPI-named mirror
+
+def MPI_Allreduce(sendbuf, recvbuf, count, datatype, op, comm):
+    return coll().MPI_Allreduce(addr(sendbuf), addr(recvbuf), count, datatype, op, _comm_handle(comm))
+
+
+def MPI_Reduce(sendbuf, recvbuf, count, datatype, op, root, comm):
+    return coll().MPI_Reduce(addr(sendbuf), addr(recvbuf), count, datatype, op, root, _comm_handle(comm))
+
+
+def MPI_Reduce_scatter(sendbuf, recvbuf, recvcnts, datatype, op, comm):
+    cn = (ctypes.c_int * len(recvcnts))(*recvcnts) if recvcnts is not None else None
+    return coll().MPI_Reduce_scatter(addr(sendbuf), addr(recvbuf), cn, datatype, op, _comm_handle(comm))
+
+
+_USER_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int),
+                            ctypes.POINTER(ctypes.c_int))
+_keepalive = []
+
+
+def MPI_Op_create(function, commute):
+    """Returns (rc, op_handle); `function(invec, inoutvec, len_ptr, type_ptr)`."""
+    cb = _USER_FN(function)
+    _keepalive.append(cb)
+    h = ctypes.c_int()
+    rc = coll().MPI_Op_create(ctypes.cast(cb, ctypes.c_void_p), commute, ctypes.byref(h))
+    return rc, h.value
+
+
+def MPI_Op_free(op):
+    """Returns (rc, new_handle)."""
+    h = ctypes.c_int(op)
+    rc = coll().MPI_Op_free(ctypes.byref(h))
+    return rc, h.value
+
+
+def MPIR_call(name, invec, inoutvec, length, datatype):
+    """Call a predefined op through its MPI_User_function symbol (e.g. "MPIR_SUM")."""
+    ln = ctypes.c_int(length)
+    dt = ctypes.c_int(datatype)
+    getattr(coll(), name)(addr(invec), addr(inoutvec), ctypes.byref(ln), ctypes.byref(dt))
+
+
+def op_errno():
+    return coll().mvx_op_errno()

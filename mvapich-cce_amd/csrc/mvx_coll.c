@@ -1,0 +1,672 @@
+/*
+ * mvx_coll.c -- libmvx.so: the MPI reduction API of the reference, run on
+ * MI355X.  Host code in C; device work goes through the C-ABI of
+ * libmvx_hip.so (include/mvx_hip.h) and RCCL (one process per GPU, xGMI).
+ *
+ * Reference call stacks replaced:
+ *   MPI_Allreduce (allreduce.c:57-92) -> collops->Allreduce -> intra_Allreduce
+ *   MPI_Reduce    (reduce.c:62-96)    -> collops->Reduce    -> intra_Reduce
+ *   MPI_Reduce_scatter (red_scat.c:60-90) -> intra_Reduce_scatter
+ * Argument checks keep the reference's order and codes (mpi_error.h,
+ * nerrmsg.c:181: code = class | kind << 6 | ring_id << 13 for messages
+ * created through MPIR_Err_setmsg).  The collective itself runs the plan of
+ * mvx_plan.c: RCCL grouped send/recv for the exchanges, one combine kernel
+ * in the reference's order for the arithmetic.
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <hip/hip_runtime_api.h>
+#include <rccl/rccl.h>
+
+#include "mvx_coll.h"
+#include "mvx_hip.h"
+
+/* ---------------------------------------------------------------------- */
+/* error codes                                                            */
+
+#define ERR_KIND_DEFAULT 1      /* MPIR_ERR_DEFAULT, mpi_error.h:119 */
+#define ERR_KIND_ALIAS 7        /* MPIR_ERR_BUFFER_ALIAS, mpi_error.h:127 */
+#define ERR_KIND_ROOT_TOOBIG 3  /* mpi_error.h:169 */
+#define ERR_TYPE_NULL_CODE MVX_ERRCLASS_TO_CODE(MPI_ERR_TYPE, 5)  /* 323 */
+#define ERR_COMM_NULL_CODE MVX_ERRCLASS_TO_CODE(MPI_ERR_COMM, 3)  /* 197 */
+
+static int g_err_ring = 1;   /* error_big_ring_pos, nerrmsg.c:75 */
+
+/* MPIR_Err_setmsg's return value (nerrmsg.c:111-182) */
+static int setmsg_code(int cls, int kind)
+{
+    int id = g_err_ring++;
+    if (g_err_ring > 8192) g_err_ring = 1;
+    return cls | (kind << MVX_ERR_CLASS_BITS) | (id << 13);
+}
+
+int MPI_Error_class(int errorcode, int *errorclass)
+{
+    if (errorclass) *errorclass = errorcode & ((1 << MVX_ERR_CLASS_BITS) - 1);
+    return MPI_SUCCESS;
+}
+
+/* ---------------------------------------------------------------------- */
+/* communicators                                                          */
+
+#define MAX_COMMS 32
+#define COMM_HANDLE_BASE 1000
+
+typedef struct {
+    int used, rank, size, device, local;
+    MPI_Comm handle;
+    ncclComm_t nccl;
+    hipStream_t stream;
+    char *pool;          /* plan staging (received shards, temporaries) */
+    size_t pool_bytes;
+    char *hpool;         /* host-buffer staging */
+    size_t hpool_bytes;
+} mvx_comm_t;
+
+static mvx_comm_t g_comms[MAX_COMMS];
+static int g_have_world = 0;
+
+static mvx_comm_t *get_comm(MPI_Comm h)
+{
+    int i;
+    for (i = 0; i < MAX_COMMS; i++)
+        if (g_comms[i].used && g_comms[i].handle == h) return &g_comms[i];
+    return NULL;
+}
+
+static mvx_comm_t *new_comm(MPI_Comm *out)
+{
+    int i;
+    for (i = 0; i < MAX_COMMS; i++) {
+        if (!g_comms[i].used) {
+            memset(&g_comms[i], 0, sizeof g_comms[i]);
+            g_comms[i].used = 1;
+            g_comms[i].handle = g_have_world ? COMM_HANDLE_BASE + i : MPI_COMM_WORLD;
+            g_have_world = 1;
+            *out = g_comms[i].handle;
+            return &g_comms[i];
+        }
+    }
+    return NULL;
+}
+
+int mvx_get_unique_id(void *id_out)
+{
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) return MPI_ERR_OTHER;
+    memcpy(id_out, &id, MVX_UNIQUE_ID_BYTES);
+    return MPI_SUCCESS;
+}
+
+int mvx_comm_init(MPI_Comm *comm, int rank, int size, int device,
+                  const void *unique_id)
+{
+    ncclUniqueId id;
+    mvx_comm_t *c;
+    if (!comm || size < 1 || size > MVX_MAXP || rank < 0 || rank >= size)
+        return MPI_ERR_ARG;
+    if (hipSetDevice(device) != hipSuccess) return MPI_ERR_OTHER;
+    c = new_comm(comm);
+    if (!c) return MPI_ERR_INTERN;
+    c->rank = rank; c->size = size; c->device = device; c->local = 0;
+    memcpy(&id, unique_id, MVX_UNIQUE_ID_BYTES);
+    if (ncclCommInitRank(&c->nccl, size, id, rank) != ncclSuccess) {
+        c->used = 0;
+        return MPI_ERR_OTHER;
+    }
+    return MPI_SUCCESS;
+}
+
+int mvx_comm_init_local(MPI_Comm *comm, int size, int device)
+{
+    mvx_comm_t *c;
+    if (!comm || size < 1 || size > MVX_MAXP) return MPI_ERR_ARG;
+    if (hipSetDevice(device) != hipSuccess) return MPI_ERR_OTHER;
+    c = new_comm(comm);
+    if (!c) return MPI_ERR_INTERN;
+    c->rank = 0; c->size = size; c->device = device; c->local = 1;
+    return MPI_SUCCESS;
+}
+
+int mvx_comm_free(MPI_Comm *comm)
+{
+    mvx_comm_t *c = comm ? get_comm(*comm) : NULL;
+    if (!c) return ERR_COMM_NULL_CODE;
+    if (c->nccl) ncclCommDestroy(c->nccl);
+    if (c->pool) hipFree(c->pool);
+    if (c->hpool) hipFree(c->hpool);
+    if (c->handle == MPI_COMM_WORLD) g_have_world = 0;
+    memset(c, 0, sizeof *c);
+    *comm = 0;
+    return MPI_SUCCESS;
+}
+
+int MPI_Comm_size(MPI_Comm comm, int *size)
+{
+    mvx_comm_t *c = get_comm(comm);
+    if (!c) return ERR_COMM_NULL_CODE;
+    *size = c->size;
+    return MPI_SUCCESS;
+}
+
+int MPI_Comm_rank(MPI_Comm comm, int *rank)
+{
+    mvx_comm_t *c = get_comm(comm);
+    if (!c) return ERR_COMM_NULL_CODE;
+    *rank = c->rank;
+    return MPI_SUCCESS;
+}
+
+int mvx_comm_set_stream(MPI_Comm comm, void *stream)
+{
+    mvx_comm_t *c = get_comm(comm);
+    if (!c) return ERR_COMM_NULL_CODE;
+    c->stream = (hipStream_t)stream;
+    return MPI_SUCCESS;
+}
+
+static int grow(char **buf, size_t *have, size_t need)
+{
+    if (need <= *have) return MPI_SUCCESS;
+    if (*buf) { hipDeviceSynchronize(); hipFree(*buf); *buf = NULL; *have = 0; }
+    need = (need + (1 << 20) - 1) & ~(size_t)((1 << 20) - 1);
+    if (hipMalloc((void **)buf, need) != hipSuccess) { *buf = NULL; return MPI_ERR_OTHER; }
+    *have = need;
+    return MPI_SUCCESS;
+}
+
+int mvx_comm_reserve(MPI_Comm comm, size_t bytes)
+{
+    mvx_comm_t *c = get_comm(comm);
+    if (!c) return ERR_COMM_NULL_CODE;
+    return grow(&c->pool, &c->pool_bytes, bytes);
+}
+
+/* ---------------------------------------------------------------------- */
+/* ops                                                                    */
+
+#define MAX_USER_OPS 64
+#define USER_OP_BASE 200
+typedef struct {           /* struct MPIR_OP, include/mpiops.h:1-11 */
+    MPI_User_function *op;
+    unsigned cookie;
+    int commute, permanent;
+} mvx_op_t;
+static mvx_op_t g_user_ops[MAX_USER_OPS];
+#define OP_COOKIE 0xca01beafu
+
+static int predefined(MPI_Op op) { return op >= MPI_MAX && op <= MPI_MAXLOC; }
+
+static mvx_op_t *user_op(MPI_Op op)
+{
+    int i = op - USER_OP_BASE;
+    if (i < 0 || i >= MAX_USER_OPS || g_user_ops[i].cookie != OP_COOKIE) return NULL;
+    return &g_user_ops[i];
+}
+
+int MPI_Op_create(MPI_User_function *function, int commute, MPI_Op *op)
+{
+    int i;
+    for (i = 0; i < MAX_USER_OPS; i++) {
+        if (g_user_ops[i].cookie != OP_COOKIE) {
+            g_user_ops[i].op = function;
+            g_user_ops[i].cookie = OP_COOKIE;
+            g_user_ops[i].commute = commute;
+            g_user_ops[i].permanent = 0;
+            *op = USER_OP_BASE + i;
+            return MPI_SUCCESS;
+        }
+    }
+    return MPI_ERR_INTERN;
+}
+
+int MPI_Op_free(MPI_Op *op)  /* opfree.c:51-82 */
+{
+    mvx_op_t *o;
+    if (!op) return MPI_ERR_ARG;
+    if (*op == MPI_OP_NULL) return MVX_ERR_OP_NULL;
+    if (predefined(*op)) return MVX_ERR_PERM_OP;
+    o = user_op(*op);
+    if (!o) return MPI_ERR_OP;
+    memset(o, 0, sizeof *o);
+    *op = MPI_OP_NULL;
+    return MPI_SUCCESS;
+}
+
+/* The op's verdict on (op, type) before any data moves: 0, 329 (undefined
+ * pair, reported only by ranks that call the op), MPI_ERR_TYPE (no device
+ * representation), MPI_ERR_OP (bad handle; user ops have no device path). */
+static int op_verdict(MPI_Op op, MPI_Datatype dt)
+{
+    if (!predefined(op)) return MPI_ERR_OP;
+    return mvx_op_apply(op, dt, NULL, NULL, 0, NULL);
+}
+
+/* ---------------------------------------------------------------------- */
+/* buffers                                                                */
+
+static int is_device_ptr(const void *p)
+{
+    hipPointerAttribute_t a;
+    if (!p) return 0;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return a.type == hipMemoryTypeDevice || a.isManaged;
+}
+
+/* staging slot base with the same alignment mod 16 as `like`, so the
+ * combine kernel keeps its 16-byte vector path */
+static size_t slot_at(size_t cur, const void *like)
+{
+    size_t base = (cur + 255) & ~(size_t)255;
+    return base + ((uintptr_t)like & 15);
+}
+
+#define NCCL_OK(x) do { if ((x) != ncclSuccess) return MPI_ERR_OTHER; } while (0)
+
+static int combine(const mvx_plan *P, const char *const *leafp, void *dst,
+                   hipStream_t st)
+{
+    const void *srcs[MVX_COMBINE_KMAX], *fold[MVX_COMBINE_KMAX];
+    int q;
+    if (P->k > MVX_COMBINE_KMAX) return MPI_ERR_INTERN;  /* p > 8 per node */
+    for (q = 0; q < P->k; q++) {
+        srcs[q] = leafp[P->leaf[q]];
+        fold[q] = P->leaf_fold[q] >= 0 ? leafp[P->leaf_fold[q]] : NULL;
+    }
+    return mvx_op_combine(P->op, P->dtype, srcs, fold, P->k, P->shape, dst,
+                          (size_t)P->c_cnt, st);
+}
+
+/* run one rank's plan over RCCL */
+static int exec_plan(mvx_comm_t *c, const mvx_plan *P, const char *sendbuf,
+                     char *recvbuf, hipStream_t st)
+{
+    const long E = P->esize;
+    size_t need = 0, slot[MVX_MAXP], tmp_off = 0;
+    const char *like = sendbuf + P->c_src_off * E;
+    const char *leafp[MVX_MAXP];
+    char *out;
+    int s, any, rc;
+
+    for (s = 0; s < P->p; s++) {
+        slot[s] = 0;
+        if (P->a_recv[s].cnt) { slot[s] = slot_at(need, like); need = slot[s] + P->a_recv[s].cnt * E; }
+    }
+    if (P->c_dst_tmp) { tmp_off = slot_at(need, like); need = tmp_off + P->c_cnt * E; }
+    if ((rc = grow(&c->pool, &c->pool_bytes, need))) return rc;
+
+    /* phase A: shards to their combining rank */
+    any = 0;
+    for (s = 0; s < P->p; s++) any |= (P->a_send[s].cnt || P->a_recv[s].cnt);
+    if (any) {
+        NCCL_OK(ncclGroupStart());
+        for (s = 0; s < P->p; s++) {
+            if (P->a_send[s].cnt)
+                NCCL_OK(ncclSend(sendbuf + P->a_send[s].off * E, (size_t)(P->a_send[s].cnt * E),
+                                 ncclUint8, s, c->nccl, st));
+            if (P->a_recv[s].cnt)
+                NCCL_OK(ncclRecv(c->pool + slot[s], (size_t)(P->a_recv[s].cnt * E),
+                                 ncclUint8, s, c->nccl, st));
+        }
+        NCCL_OK(ncclGroupEnd());
+    }
+    /* phase B: the reference's whole combine tree for this rank's block */
+    out = P->c_dst_tmp ? c->pool + tmp_off : recvbuf + P->c_dst_off * E;
+    if (P->has_combine && P->c_cnt > 0) {
+        for (s = 0; s < P->p; s++)
+            leafp[s] = (s == P->rank) ? sendbuf + P->c_src_off * E : c->pool + slot[s];
+        if ((rc = combine(P, leafp, out, st))) return rc;
+    }
+    /* phase C: combined blocks to the ranks that need them */
+    any = 0;
+    for (s = 0; s < P->p; s++) any |= (P->b_send[s].cnt || P->b_recv[s].cnt);
+    if (any) {
+        NCCL_OK(ncclGroupStart());
+        for (s = 0; s < P->p; s++) {
+            if (P->b_send[s].cnt)
+                NCCL_OK(ncclSend(out, (size_t)(P->b_send[s].cnt * E), ncclUint8, s, c->nccl, st));
+            if (P->b_recv[s].cnt)
+                NCCL_OK(ncclRecv(recvbuf + P->b_recv[s].off * E, (size_t)(P->b_recv[s].cnt * E),
+                                 ncclUint8, s, c->nccl, st));
+        }
+        NCCL_OK(ncclGroupEnd());
+    }
+    return MPI_SUCCESS;
+}
+
+/* ---------------------------------------------------------------------- */
+/* collective bodies (after the API-level argument checks)                */
+
+typedef struct {
+    int coll;
+    const char *sendbuf;
+    char *recvbuf;
+    long count;           /* Allreduce / Reduce */
+    const int *recvcnts;  /* Reduce_scatter */
+    MPI_Datatype dt;
+    MPI_Op op;
+    int root;
+} call_t;
+
+/* element counts of this rank's send / recv vectors */
+static void call_sizes(const call_t *k, mvx_comm_t *c, long *nsend, long *nrecv)
+{
+    if (k->coll == MVX_COLL_REDUCE_SCATTER) {
+        long t = 0;
+        int i;
+        for (i = 0; i < c->size; i++) t += k->recvcnts[i];
+        *nsend = t;
+        *nrecv = k->recvcnts[c->rank];
+    } else {
+        *nsend = k->count;
+        *nrecv = (k->coll == MVX_COLL_REDUCE && c->rank != k->root) ? 0 : k->count;
+    }
+}
+
+static int run(mvx_comm_t *c, const call_t *k, hipStream_t st, int blocking)
+{
+    mvx_plan P;
+    int rc, verdict, sdev, rdev;
+    long nsend, nrecv;
+    int e, ts;
+
+    if (c->local) return MPI_ERR_COMM;   /* virtual comms use *_multi */
+    mvx_dtype_info(k->dt, &e, &ts);
+    rc = mvx_plan_build(&P, k->coll, c->size, c->rank, k->count, k->recvcnts,
+                        k->dt, k->op, k->root);
+    if (rc) return rc;
+    if (P.alg == MVX_ALG_NONE) return MPI_SUCCESS;
+    verdict = op_verdict(k->op, k->dt);
+    if (verdict == MVX_ERR_OP_NOT_DEFINED) return P.calls_uop ? verdict : MPI_SUCCESS;
+    if (verdict) return verdict;
+
+    call_sizes(k, c, &nsend, &nrecv);
+    sdev = nsend == 0 || is_device_ptr(k->sendbuf);
+    rdev = nrecv == 0 || is_device_ptr(k->recvbuf);
+    if (sdev && rdev) {
+        rc = exec_plan(c, &P, k->sendbuf, k->recvbuf, st);
+        if (rc == MPI_SUCCESS && blocking && hipStreamSynchronize(st) != hipSuccess)
+            rc = MPI_ERR_OTHER;
+        return rc;
+    }
+    if (!blocking) return MPI_ERR_BUFFER;
+    {   /* host buffers: stage through HBM (H2D, device collective, D2H) */
+        const size_t sb = (size_t)(nsend * e), rb = (size_t)(nrecv * e);
+        const size_t roff = (sb + 255) & ~(size_t)255;
+        char *ds, *dr;
+        if ((rc = grow(&c->hpool, &c->hpool_bytes, roff + rb + 256))) return rc;
+        ds = sdev ? (char *)k->sendbuf : c->hpool;
+        dr = rdev ? k->recvbuf : c->hpool + roff;
+        if (!sdev && sb && hipMemcpyAsync(ds, k->sendbuf, sb, hipMemcpyHostToDevice, st) != hipSuccess)
+            return MPI_ERR_OTHER;
+        rc = exec_plan(c, &P, ds, dr, st);
+        if (rc) return rc;
+        if (!rdev && rb && hipMemcpyAsync(k->recvbuf, dr, rb, hipMemcpyDeviceToHost, st) != hipSuccess)
+            return MPI_ERR_OTHER;
+        return hipStreamSynchronize(st) == hipSuccess ? MPI_SUCCESS : MPI_ERR_OTHER;
+    }
+}
+
+/* ---------------------------------------------------------------------- */
+/* MPI API                                                                */
+
+int MPI_Allreduce(void *sendbuf, void *recvbuf, int count, MPI_Datatype dt,
+                  MPI_Op op, MPI_Comm comm)
+{
+    mvx_comm_t *c = get_comm(comm);
+    call_t k;
+    if (!c) return ERR_COMM_NULL_CODE;                       /* TEST_MPI_COMM */
+    if (mvx_dtype_info(dt, NULL, NULL)) return ERR_TYPE_NULL_CODE;  /* TEST_DTYPE */
+    if (count < 0) return setmsg_code(MPI_ERR_COUNT, ERR_KIND_DEFAULT);
+    if (sendbuf == recvbuf) return setmsg_code(MPI_ERR_BUFFER, ERR_KIND_ALIAS);
+    if (count == 0) return MPI_SUCCESS;                     /* 5479 */
+    if (!predefined(op) && !user_op(op)) return MPI_ERR_OP; /* TEST_MPI_OP */
+    k.coll = MVX_COLL_ALLREDUCE; k.sendbuf = sendbuf; k.recvbuf = recvbuf;
+    k.count = count; k.recvcnts = NULL; k.dt = dt; k.op = op; k.root = 0;
+    return run(c, &k, c->stream, 1);
+}
+
+int MPI_Reduce(void *sendbuf, void *recvbuf, int count, MPI_Datatype dt,
+               MPI_Op op, int root, MPI_Comm comm)
+{
+    mvx_comm_t *c = get_comm(comm);
+    call_t k;
+    int rc = 0;
+    if (!c) return ERR_COMM_NULL_CODE;
+    if (mvx_dtype_info(dt, NULL, NULL)) return ERR_TYPE_NULL_CODE;
+    if (sendbuf == recvbuf) return setmsg_code(MPI_ERR_BUFFER, ERR_KIND_ALIAS);
+    if (count < 0) return setmsg_code(MPI_ERR_COUNT, ERR_KIND_DEFAULT);
+    if (count == 0) return MPI_SUCCESS;                     /* 4541 */
+    if (root >= c->size) rc = setmsg_code(MPI_ERR_ROOT, ERR_KIND_ROOT_TOOBIG);
+    if (root < 0) rc = setmsg_code(MPI_ERR_ROOT, ERR_KIND_DEFAULT);
+    if (rc) return rc;
+    if (!predefined(op) && !user_op(op)) return MPI_ERR_OP;
+    k.coll = MVX_COLL_REDUCE; k.sendbuf = sendbuf; k.recvbuf = recvbuf;
+    k.count = count; k.recvcnts = NULL; k.dt = dt; k.op = op; k.root = root;
+    return run(c, &k, c->stream, 1);
+}
+
+int MPI_Reduce_scatter(void *sendbuf, void *recvbuf, int *recvcnts,
+                       MPI_Datatype dt, MPI_Op op, MPI_Comm comm)
+{
+    mvx_comm_t *c = get_comm(comm);
+    call_t k;
+    if (!c) return ERR_COMM_NULL_CODE;
+    if (mvx_dtype_info(dt, NULL, NULL)) return ERR_TYPE_NULL_CODE;
+    if (recvbuf == sendbuf) return setmsg_code(MPI_ERR_BUFFER, ERR_KIND_ALIAS);
+    if (!predefined(op) && !user_op(op)) return MPI_ERR_OP;
+    if (!recvcnts) return MPI_ERR_ARG;
+    k.coll = MVX_COLL_REDUCE_SCATTER; k.sendbuf = sendbuf; k.recvbuf = recvbuf;
+    k.count = 0; k.recvcnts = recvcnts; k.dt = dt; k.op = op; k.root = 0;
+    return run(c, &k, c->stream, 1);
+}
+
+int PMPI_Reduce(void *a, void *b, int n, MPI_Datatype d, MPI_Op o, int r, MPI_Comm c)
+{ return MPI_Reduce(a, b, n, d, o, r, c); }
+int PMPI_Allreduce(void *a, void *b, int n, MPI_Datatype d, MPI_Op o, MPI_Comm c)
+{ return MPI_Allreduce(a, b, n, d, o, c); }
+int PMPI_Reduce_scatter(void *a, void *b, int *n, MPI_Datatype d, MPI_Op o, MPI_Comm c)
+{ return MPI_Reduce_scatter(a, b, n, d, o, c); }
+int PMPI_Op_create(MPI_User_function *f, int cm, MPI_Op *o) { return MPI_Op_create(f, cm, o); }
+int PMPI_Op_free(MPI_Op *o) { return MPI_Op_free(o); }
+
+const mvx_collops MVX_device_collops = { MPI_Reduce, MPI_Allreduce, MPI_Reduce_scatter };
+
+/* stream-ordered variants: device buffers, no host synchronisation */
+static int async_checks(mvx_comm_t *c, MPI_Datatype dt, MPI_Op op)
+{
+    if (!c) return ERR_COMM_NULL_CODE;
+    if (mvx_dtype_info(dt, NULL, NULL)) return ERR_TYPE_NULL_CODE;
+    if (!predefined(op) && !user_op(op)) return MPI_ERR_OP;
+    return MPI_SUCCESS;
+}
+
+int mvx_allreduce_async(const void *sendbuf, void *recvbuf, int count,
+                        MPI_Datatype dt, MPI_Op op, MPI_Comm comm, void *stream)
+{
+    mvx_comm_t *c = get_comm(comm);
+    call_t k;
+    int rc = async_checks(c, dt, op);
+    if (rc) return rc;
+    if (count < 0) return MPI_ERR_COUNT;
+    if (sendbuf == recvbuf) return MPI_ERR_BUFFER;
+    k.coll = MVX_COLL_ALLREDUCE; k.sendbuf = sendbuf; k.recvbuf = recvbuf;
+    k.count = count; k.recvcnts = NULL; k.dt = dt; k.op = op; k.root = 0;
+    return run(c, &k, (hipStream_t)stream, 0);
+}
+
+int mvx_reduce_async(const void *sendbuf, void *recvbuf, int count,
+                     MPI_Datatype dt, MPI_Op op, int root, MPI_Comm comm, void *stream)
+{
+    mvx_comm_t *c = get_comm(comm);
+    call_t k;
+    int rc = async_checks(c, dt, op);
+    if (rc) return rc;
+    if (count < 0) return MPI_ERR_COUNT;
+    if (root < 0 || root >= c->size) return MPI_ERR_ROOT;
+    if (sendbuf == recvbuf) return MPI_ERR_BUFFER;
+    k.coll = MVX_COLL_REDUCE; k.sendbuf = sendbuf; k.recvbuf = recvbuf;
+    k.count = count; k.recvcnts = NULL; k.dt = dt; k.op = op; k.root = root;
+    return run(c, &k, (hipStream_t)stream, 0);
+}
+
+int mvx_reduce_scatter_async(const void *sendbuf, void *recvbuf, const int *recvcnts,
+                             MPI_Datatype dt, MPI_Op op, MPI_Comm comm, void *stream)
+{
+    mvx_comm_t *c = get_comm(comm);
+    call_t k;
+    int rc = async_checks(c, dt, op);
+    if (rc) return rc;
+    if (!recvcnts) return MPI_ERR_ARG;
+    if (sendbuf == recvbuf) return MPI_ERR_BUFFER;
+    k.coll = MVX_COLL_REDUCE_SCATTER; k.sendbuf = sendbuf; k.recvbuf = recvbuf;
+    k.count = 0; k.recvcnts = recvcnts; k.dt = dt; k.op = op; k.root = 0;
+    return run(c, &k, (hipStream_t)stream, 0);
+}
+
+/* ---------------------------------------------------------------------- */
+/* virtual communicators: every rank's plan on one device                 */
+
+static int run_multi(mvx_comm_t *c, int coll, void *const *sendbufs,
+                     void *const *recvbufs, long count, const int *recvcnts,
+                     MPI_Datatype dt, MPI_Op op, int root, int *rcs,
+                     hipStream_t st)
+{
+    static mvx_plan plans[MVX_MAXP];
+    const int p = c->size;
+    int r, s, rc, verdict, e, ts;
+    size_t need = 0, tmp_off[MVX_MAXP];
+
+    if (mvx_dtype_info(dt, &e, &ts)) return ERR_TYPE_NULL_CODE;
+    for (r = 0; r < p; r++) rcs[r] = 0;
+    if (!predefined(op) && !user_op(op)) { for (r = 0; r < p; r++) rcs[r] = MPI_ERR_OP; return MPI_SUCCESS; }
+    for (r = 0; r < p; r++) {
+        rc = mvx_plan_build(&plans[r], coll, p, r, count, recvcnts, dt, op, root);
+        if (rc) return rc;
+    }
+    if (plans[0].alg == MVX_ALG_NONE) return MPI_SUCCESS;
+    verdict = op_verdict(op, dt);
+    if (verdict) {
+        for (r = 0; r < p; r++)
+            rcs[r] = (verdict == MVX_ERR_OP_NOT_DEFINED && !plans[r].calls_uop) ? 0 : verdict;
+        return MPI_SUCCESS;
+    }
+    for (r = 0; r < p; r++) {
+        long nsend = plans[r].count, nrecv;
+        nrecv = coll == MVX_COLL_REDUCE_SCATTER ? recvcnts[r]
+              : (coll == MVX_COLL_REDUCE && r != root) ? 0 : count;
+        if ((nsend && !is_device_ptr(sendbufs[r])) || (nrecv && !is_device_ptr(recvbufs[r])))
+            return MPI_ERR_BUFFER;
+        if (sendbufs[r] == recvbufs[r]) return MPI_ERR_BUFFER;
+        tmp_off[r] = 0;
+        if (plans[r].c_dst_tmp) {
+            tmp_off[r] = slot_at(need, (const char *)sendbufs[r] + plans[r].c_src_off * e);
+            need = tmp_off[r] + plans[r].c_cnt * e;
+        }
+    }
+    if ((rc = grow(&c->pool, &c->pool_bytes, need))) return rc;
+    /* phase A is free: leaves read the other ranks' sendbufs directly */
+    for (r = 0; r < p; r++) {
+        const mvx_plan *P = &plans[r];
+        const char *leafp[MVX_MAXP];
+        char *out;
+        if (!P->has_combine || P->c_cnt == 0) continue;
+        for (s = 0; s < p; s++) leafp[s] = (const char *)sendbufs[s] + P->c_src_off * e;
+        out = P->c_dst_tmp ? c->pool + tmp_off[r] : (char *)recvbufs[r] + P->c_dst_off * e;
+        if ((rc = combine(P, leafp, out, st))) return rc;
+    }
+    /* phase C: device-to-device copies */
+    for (r = 0; r < p; r++) {
+        const mvx_plan *P = &plans[r];
+        const char *out = P->c_dst_tmp ? c->pool + tmp_off[r]
+                                       : (const char *)recvbufs[r] + P->c_dst_off * e;
+        for (s = 0; s < p; s++) {
+            if (!P->b_send[s].cnt) continue;
+            if (hipMemcpyAsync((char *)recvbufs[s] + P->b_send[s].off * e, out,
+                               (size_t)(P->b_send[s].cnt * e), hipMemcpyDeviceToDevice,
+                               st) != hipSuccess)
+                return MPI_ERR_OTHER;
+        }
+    }
+    return MPI_SUCCESS;
+}
+
+int mvx_allreduce_multi(void *const *sendbufs, void *const *recvbufs, int count,
+                        MPI_Datatype dt, MPI_Op op, MPI_Comm comm, int *rc, void *stream)
+{
+    mvx_comm_t *c = get_comm(comm);
+    if (!c || !c->local) return ERR_COMM_NULL_CODE;
+    if (count < 0) return MPI_ERR_COUNT;
+    return run_multi(c, MVX_COLL_ALLREDUCE, sendbufs, recvbufs, count, NULL, dt, op,
+                     0, rc, (hipStream_t)stream);
+}
+
+int mvx_reduce_multi(void *const *sendbufs, void *const *recvbufs, int count,
+                     MPI_Datatype dt, MPI_Op op, int root, MPI_Comm comm, int *rc,
+                     void *stream)
+{
+    mvx_comm_t *c = get_comm(comm);
+    if (!c || !c->local) return ERR_COMM_NULL_CODE;
+    if (count < 0) return MPI_ERR_COUNT;
+    if (root < 0 || root >= c->size) return MPI_ERR_ROOT;
+    return run_multi(c, MVX_COLL_REDUCE, sendbufs, recvbufs, count, NULL, dt, op,
+                     root, rc, (hipStream_t)stream);
+}
+
+int mvx_reduce_scatter_multi(void *const *sendbufs, void *const *recvbufs,
+                             const int *recvcnts, MPI_Datatype dt, MPI_Op op,
+                             MPI_Comm comm, int *rc, void *stream)
+{
+    mvx_comm_t *c = get_comm(comm);
+    if (!c || !c->local) return ERR_COMM_NULL_CODE;
+    if (!recvcnts) return MPI_ERR_ARG;
+    return run_multi(c, MVX_COLL_REDUCE_SCATTER, sendbufs, recvbufs, 0, recvcnts, dt,
+                     op, 0, rc, (hipStream_t)stream);
+}
+
+/* ---------------------------------------------------------------------- */
+/* the predefined ops as MPI_User_functions                               */
+
+static int g_op_errno = 0;   /* MPIR_Op_errno, global_ops.c:41 */
+
+int mvx_op_errno(void)
+{
+    int e = g_op_errno;
+    g_op_errno = 0;
+    return e;
+}
+
+static void uop_call(MPI_Op op, void *in, void *inout, int *len, MPI_Datatype *t)
+{
+    int rc;
+    if (!len || !t) { g_op_errno = MPI_ERR_ARG; return; }
+    rc = mvx_op_apply(op, *t, NULL, NULL, 0, NULL);   /* verdict first */
+    if (rc == MPI_SUCCESS && *len > 0) {
+        if (!is_device_ptr(in) || !is_device_ptr(inout)) rc = MPI_ERR_BUFFER;
+        else {
+            rc = mvx_op_apply(op, *t, in, inout, (size_t)*len, NULL);
+            if (rc == MPI_SUCCESS && hipStreamSynchronize(NULL) != hipSuccess) rc = MPI_ERR_OTHER;
+        }
+    }
+    if (rc) g_op_errno = rc;
+}
+
+#define UOP(NAME, OPH) \
+    void NAME(void *in, void *io, int *len, MPI_Datatype *t) { uop_call(OPH, in, io, len, t); }
+UOP(MPIR_MAXF, MPI_MAX)
+UOP(MPIR_MINF, MPI_MIN)
+UOP(MPIR_SUM, MPI_SUM)
+UOP(MPIR_PROD, MPI_PROD)
+UOP(MPIR_LAND, MPI_LAND)
+UOP(MPIR_BAND, MPI_BAND)
+UOP(MPIR_LOR, MPI_LOR)
+UOP(MPIR_BOR, MPI_BOR)
+UOP(MPIR_LXOR, MPI_LXOR)
+UOP(MPIR_BXOR, MPI_BXOR)
+UOP(MPIR_MAXLOC, MPI_MAXLOC)
+UOP(MPIR_MINLOC, MPI_MINLOC)

@@ -1,0 +1,538 @@
+// mvx_ops.hip -- the device side of the MPI local reduction path, written for
+// gfx950 (CDNA4, wave64).  Built into libmvx_hip.so; C-ABI in
+// include/mvx_hip.h.
+//
+// One kernel template covers every predefined op x type of the reference
+// (src/coll/global_ops.c:56-1745) and every combine order of its collectives
+// (src/coll/intra_fns_new.c): a launch reads k leaf operands (optionally each
+// pre-folded with a partner, the non-power-of-two fold of intra_fns_new.c
+// 5548-5577 / 4641-4671 / 6283-6312), reduces them in registers in a TREE or
+// CHAIN shape whose left operand always plays the reference's `inoutvec`
+// role, and writes the result once.  A k-way combine is one HBM pass instead
+// of the reference's log2(p) or p-1 passes over the block.
+//
+// Element-wise: no MFMA, no LDS.  Every lane moves 16 bytes per operand per
+// chunk (global_load_dwordx4), chunks are lane-contiguous so a wave touches
+// 1 KiB per load instruction, several chunks per lane are in flight before
+// the first use, and the store is one dwordx4 per chunk.  Pair types
+// (MAXLOC/MINLOC) are 8 or 16 bytes, so a 16-byte lane load always holds
+// whole pairs: no LDS transposition is needed.
+//
+// Numerics follow the reference's x86-64 gcc -O2 build: IEEE round-to-nearest
+// f32/f64 with denormals (no flush), no contraction (-ffp-contract=off keeps
+// the complex product of global_ops.c:518-519 unfused), MAX/MIN as the
+// select `(b > a) ? b : a` of coll.h:14-19 (not v_max: NaN and signed-zero
+// roles matter), integer arithmetic in unsigned form (the reference's signed
+// wrap, without UB).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include "mvx_mpi.h"
+#include "mvx_hip.h"
+
+namespace mvx {
+
+enum { OMAX = 0, OMIN, OSUM, OPROD, OLAND, OBAND, OLOR, OBOR, OLXOR, OBXOR,
+       OMINLOC, OMAXLOC };
+
+// Element layouts: the reference's C types on x86-64 LP64.
+struct cf32 { float re, im; };                          // global_ops.c:43-46
+struct cf64 { double re, im; };                         // global_ops.c:48-51
+struct pfi { float v; int32_t l; };                     // initdte.c:74-78
+struct alignas(8) pdi { double v; int32_t l; };         // 16 B, 4 B pad
+struct alignas(8) pli { int64_t v; int32_t l; };        // 16 B, 4 B pad
+struct psi { int16_t v; int32_t l; };                   // 8 B, 2 B pad
+struct pii { int32_t v; int32_t l; };                   // MPI_2INT
+static_assert(sizeof(pdi) == 16 && sizeof(pli) == 16 && sizeof(psi) == 8, "");
+
+template <typename T> struct is_pair { static constexpr bool value = false; };
+template <> struct is_pair<pfi> { static constexpr bool value = true; };
+template <> struct is_pair<pdi> { static constexpr bool value = true; };
+template <> struct is_pair<pli> { static constexpr bool value = true; };
+template <> struct is_pair<psi> { static constexpr bool value = true; };
+template <> struct is_pair<pii> { static constexpr bool value = true; };
+
+// ---------------------------------------------------------------------------
+// the ops: F<op, T>::f(a, b) returns the new inout value (a = inout, b = in)
+
+template <int O, typename T> struct F;
+
+template <typename T> struct F<OMAX, T> {     // coll.h:17-18
+    static __device__ __forceinline__ T f(T a, T b) { return (b > a) ? b : a; }
+};
+template <typename T> struct F<OMIN, T> {     // coll.h:14-15
+    static __device__ __forceinline__ T f(T a, T b) { return (a > b) ? b : a; }
+};
+
+template <typename T> __device__ __forceinline__ T add_(T a, T b) { return (T)(a + b); }
+template <typename T> __device__ __forceinline__ T mul_(T a, T b) { return (T)(a * b); }
+// promote narrow unsigned before multiplying so the product cannot overflow int
+template <> __device__ __forceinline__ uint8_t mul_(uint8_t a, uint8_t b)
+{ return (uint8_t)((uint32_t)a * (uint32_t)b); }
+template <> __device__ __forceinline__ uint16_t mul_(uint16_t a, uint16_t b)
+{ return (uint16_t)((uint32_t)a * (uint32_t)b); }
+
+template <typename T> struct F<OSUM, T> {
+    static __device__ __forceinline__ T f(T a, T b) { return add_(a, b); }
+};
+template <> struct F<OSUM, cf32> {
+    static __device__ __forceinline__ cf32 f(cf32 a, cf32 b)
+    { cf32 r; r.re = a.re + b.re; r.im = a.im + b.im; return r; }
+};
+template <> struct F<OSUM, cf64> {
+    static __device__ __forceinline__ cf64 f(cf64 a, cf64 b)
+    { cf64 r; r.re = a.re + b.re; r.im = a.im + b.im; return r; }
+};
+template <typename T> struct F<OPROD, T> {
+    static __device__ __forceinline__ T f(T a, T b) { return mul_(a, b); }
+};
+template <> struct F<OPROD, cf32> {            // global_ops.c:513-521
+    static __device__ __forceinline__ cf32 f(cf32 c, cf32 b)
+    { cf32 r; r.re = c.re * b.re - c.im * b.im; r.im = c.im * b.re + c.re * b.im; return r; }
+};
+template <> struct F<OPROD, cf64> {            // global_ops.c:523-531
+    static __device__ __forceinline__ cf64 f(cf64 c, cf64 b)
+    { cf64 r; r.re = c.re * b.re - c.im * b.im; r.im = c.im * b.re + c.re * b.im; return r; }
+};
+template <typename T> struct F<OLAND, T> {
+    static __device__ __forceinline__ T f(T a, T b) { return (a != T(0) && b != T(0)) ? T(1) : T(0); }
+};
+template <typename T> struct F<OLOR, T> {
+    static __device__ __forceinline__ T f(T a, T b) { return (a != T(0) || b != T(0)) ? T(1) : T(0); }
+};
+template <typename T> struct F<OLXOR, T> {
+    static __device__ __forceinline__ T f(T a, T b) { return ((a != T(0)) != (b != T(0))) ? T(1) : T(0); }
+};
+template <typename T> struct F<OBAND, T> {
+    static __device__ __forceinline__ T f(T a, T b) { return (T)(a & b); }
+};
+template <typename T> struct F<OBOR, T> {
+    static __device__ __forceinline__ T f(T a, T b) { return (T)(a | b); }
+};
+template <typename T> struct F<OBXOR, T> {
+    static __device__ __forceinline__ T f(T a, T b) { return (T)(a ^ b); }
+};
+// MAXLOC / MINLOC: global_ops.c:1297-1309 and 1524-1536.  Fields are written
+// one by one so the padding bytes of `a` survive (the reference writes only
+// value and loc).
+template <typename T> struct F<OMAXLOC, T> {
+    static __device__ __forceinline__ T f(T a, T b) {
+        if (a.v == b.v) a.l = (a.l > b.l) ? b.l : a.l;
+        else if (a.v < b.v) { a.v = b.v; a.l = b.l; }
+        return a;
+    }
+};
+template <typename T> struct F<OMINLOC, T> {
+    static __device__ __forceinline__ T f(T a, T b) {
+        if (a.v == b.v) a.l = (a.l > b.l) ? b.l : a.l;
+        else if (a.v > b.v) { a.v = b.v; a.l = b.l; }
+        return a;
+    }
+};
+
+// ---------------------------------------------------------------------------
+// launch parameters (passed by value, ~170 bytes of kernarg)
+
+struct Params {
+    const char *src[MVX_COMBINE_KMAX];
+    const char *fold[MVX_COMBINE_KMAX];
+    char *dst;
+    long n;      // elements
+    long head;   // scalar elements before the 16-byte aligned body
+    long nvec;   // 16-byte chunks in the body
+    int k;       // leaves
+    int vec_ok;  // all pointers share their alignment mod 16
+};
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));  // one dwordx4
+
+// 16 bytes of elements; moved to/from the dwordx4 registers by memcpy (a
+// well-defined bit copy that keeps pair padding bytes; union punning lets
+// clang drop the element writes).
+template <typename T> struct Chunk {
+    T e[16 / sizeof(T)];
+};
+
+template <typename T>
+__device__ __forceinline__ Chunk<T> unpack(u32x4 r)
+{
+    Chunk<T> c;
+    __builtin_memcpy(&c, &r, 16);
+    return c;
+}
+
+template <typename T>
+__device__ __forceinline__ u32x4 pack(const Chunk<T> &c)
+{
+    u32x4 r;
+    __builtin_memcpy(&r, &c, 16);
+    return r;
+}
+
+// write only the value/loc fields of a pair (its padding stays as it was)
+template <typename T>
+__device__ __forceinline__ void set_fields(T &d, const T &r)
+{
+    if constexpr (is_pair<T>::value) { d.v = r.v; d.l = r.l; }
+    else d = r;
+}
+
+template <typename T>
+__device__ __forceinline__ void store_elt(T *d, const T &r) { *d = r; }
+template <> __device__ __forceinline__ void store_elt(pdi *d, const pdi &r) { d->v = r.v; d->l = r.l; }
+template <> __device__ __forceinline__ void store_elt(pli *d, const pli &r) { d->v = r.v; d->l = r.l; }
+template <> __device__ __forceinline__ void store_elt(psi *d, const psi &r) { d->v = r.v; d->l = r.l; }
+
+template <int O, typename T, int KMAX, int SHAPE>
+__device__ __forceinline__ void reduce_leaves(T (&y)[KMAX], int k)
+{
+    if (SHAPE == MVX_SHAPE_CHAIN) {
+#pragma unroll
+        for (int q = 1; q < KMAX; ++q)
+            if (q < k) y[0] = F<O, T>::f(y[0], y[q]);
+    } else {
+#pragma unroll
+        for (int h = 1; h < KMAX; h <<= 1) {
+#pragma unroll
+            for (int q = 0; q + h < KMAX; q += 2 * h)
+                if (q + h < k) y[q] = F<O, T>::f(y[q], y[q + h]);
+        }
+    }
+}
+
+template <int O, typename T, int KMAX, int SHAPE>
+__device__ __forceinline__ void scalar_elem(const Params &P, long i)
+{
+    T y[KMAX];
+#pragma unroll
+    for (int q = 0; q < KMAX; ++q) {
+        if (q < P.k) {
+            y[q] = reinterpret_cast<const T *>(P.src[q])[i];
+            if (P.fold[q]) y[q] = F<O, T>::f(y[q], reinterpret_cast<const T *>(P.fold[q])[i]);
+        }
+    }
+    reduce_leaves<O, T, KMAX, SHAPE>(y, P.k);
+    store_elt(reinterpret_cast<T *>(P.dst) + i, y[0]);
+}
+
+// U = 16-byte chunks per lane per iteration (loads in flight per operand).
+template <int O, typename T, int KMAX, int SHAPE, int U>
+__global__ void __launch_bounds__(256)
+k_combine(const Params P)
+{
+    constexpr int V = 16 / sizeof(T);
+    const long tid = (long)blockIdx.x * 256 + threadIdx.x;
+    const long nthr = (long)gridDim.x * 256;
+
+    if (!P.vec_ok) {  // operands misaligned against each other: element loads
+        for (long i = tid; i < P.n; i += nthr) scalar_elem<O, T, KMAX, SHAPE>(P, i);
+        return;
+    }
+    {   // head and tail elements outside the aligned body
+        const long tail0 = P.head + P.nvec * V;
+        const long nscal = P.head + (P.n - tail0);
+        for (long s = tid; s < nscal; s += nthr) {
+            const long i = s < P.head ? s : tail0 + (s - P.head);
+            scalar_elem<O, T, KMAX, SHAPE>(P, i);
+        }
+    }
+    const u32x4 *src[KMAX];
+    const u32x4 *fold[KMAX];
+#pragma unroll
+    for (int q = 0; q < KMAX; ++q) {
+        src[q] = reinterpret_cast<const u32x4 *>(P.src[q] + P.head * (long)sizeof(T));
+        fold[q] = P.fold[q] ? reinterpret_cast<const u32x4 *>(P.fold[q] + P.head * (long)sizeof(T)) : nullptr;
+    }
+    u32x4 *dst = reinterpret_cast<u32x4 *>(P.dst + P.head * (long)sizeof(T));
+    const int k = P.k;
+
+    for (long c0 = (long)blockIdx.x * (256 * U) + threadIdx.x; c0 < P.nvec; c0 += nthr * U) {
+        Chunk<T> x[U][KMAX];
+        // issue every load of the iteration before the first use
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const long c = c0 + (long)u * 256;
+            if (c < P.nvec) {
+#pragma unroll
+                for (int q = 0; q < KMAX; ++q)
+                    if (q < k) x[u][q] = unpack<T>(src[q][c]);
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < KMAX; ++q) {
+            if (q < k && fold[q]) {
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const long c = c0 + (long)u * 256;
+                    if (c < P.nvec) {
+                        const Chunk<T> f = unpack<T>(fold[q][c]);
+#pragma unroll
+                        for (int j = 0; j < V; ++j) x[u][q].e[j] = F<O, T>::f(x[u][q].e[j], f.e[j]);
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const long c = c0 + (long)u * 256;
+            if (c < P.nvec) {
+#pragma unroll
+                for (int j = 0; j < V; ++j) {
+                    T y[KMAX];
+#pragma unroll
+                    for (int q = 0; q < KMAX; ++q) y[q] = x[u][q].e[j];
+                    reduce_leaves<O, T, KMAX, SHAPE>(y, k);
+                    set_fields(x[u][0].e[j], y[0]);  // keeps leaf 0's padding
+                }
+                dst[c] = pack<T>(x[u][0]);
+            }
+        }
+    }
+}
+
+}  // namespace mvx
+
+// ---------------------------------------------------------------------------
+// dispatch: (op, datatype handle) -> kernel set
+
+namespace mvx {
+
+typedef void (*KFn)(const Params);
+
+struct KSet {
+    const void *apply;  // KMAX 2 (k <= 2), 4 chunks in flight per lane
+    const void *tree;   // KMAX 8, TREE
+    const void *chain;  // KMAX 8, CHAIN
+    int esize;
+    const char *name;
+};
+
+template <int O, typename T>
+static KSet kset(const char *name)
+{
+    KSet s;
+    s.apply = (const void *)&k_combine<O, T, 2, MVX_SHAPE_CHAIN, 4>;
+    s.tree = (const void *)&k_combine<O, T, MVX_COMBINE_KMAX, MVX_SHAPE_TREE, 1>;
+    s.chain = (const void *)&k_combine<O, T, MVX_COMBINE_KMAX, MVX_SHAPE_CHAIN, 1>;
+    s.esize = (int)sizeof(T);
+    s.name = name;
+    return s;
+}
+
+// element kinds of the datatype handles (mvx_mpi.h / reference mpi.h:64-115)
+enum { EK_NONE = 0, EK_I8, EK_U8, EK_BYTE, EK_I16, EK_U16, EK_I32, EK_U32,
+       EK_I64, EK_U64, EK_F32, EK_F64, EK_C32, EK_C64, EK_PFI, EK_PDI, EK_PLI,
+       EK_PSI, EK_PII, EK_LDBL, EK_LDBL_INT };
+
+static int ekind(int dtype)
+{
+    switch (dtype) {
+    case MPI_CHAR: return EK_I8;
+    case MPI_UNSIGNED_CHAR: return EK_U8;
+    case MPI_BYTE: return EK_BYTE;
+    case MPI_SHORT: return EK_I16;
+    case MPI_UNSIGNED_SHORT: return EK_U16;
+    case MPI_INT: return EK_I32;
+    case MPI_UNSIGNED: return EK_U32;
+    case MPI_LONG: case MPI_LONG_LONG_INT: return EK_I64;
+    case MPI_UNSIGNED_LONG: return EK_U64;
+    case MPI_FLOAT: return EK_F32;
+    case MPI_DOUBLE: return EK_F64;
+    case MPI_COMPLEX: return EK_C32;
+    case MPI_DOUBLE_COMPLEX: return EK_C64;
+    case MPI_FLOAT_INT: return EK_PFI;
+    case MPI_DOUBLE_INT: return EK_PDI;
+    case MPI_LONG_INT: return EK_PLI;
+    case MPI_SHORT_INT: return EK_PSI;
+    case MPI_2INT: return EK_PII;
+    case MPI_LONG_DOUBLE: return EK_LDBL;
+    case MPI_LONG_DOUBLE_INT: return EK_LDBL_INT;
+    default: return EK_NONE;
+    }
+}
+
+static int ek_size(int ek)
+{
+    static const int sz[] = {0, 1, 1, 1, 2, 2, 4, 4, 8, 8, 4, 8, 8, 16, 8, 16, 16, 8, 8, 16, 32};
+    return sz[ek];
+}
+
+// Integer SUM/PROD/logical/bitwise results do not depend on signedness in
+// two's complement, so those share the unsigned kernel of the same width;
+// MAX/MIN compare and keep the signed kernels.
+#define ARITH_INT(O, NAME)                                                   \
+    case EK_I8: case EK_U8:   { static KSet s = kset<O, uint8_t>(NAME "_u8"); return &s; } \
+    case EK_I16: case EK_U16: { static KSet s = kset<O, uint16_t>(NAME "_u16"); return &s; } \
+    case EK_I32: case EK_U32: { static KSet s = kset<O, uint32_t>(NAME "_u32"); return &s; } \
+    case EK_I64: case EK_U64: { static KSet s = kset<O, uint64_t>(NAME "_u64"); return &s; }
+#define FLOATS(O, NAME)                                                      \
+    case EK_F32: { static KSet s = kset<O, float>(NAME "_f32"); return &s; } \
+    case EK_F64: { static KSet s = kset<O, double>(NAME "_f64"); return &s; }
+#define CMPLX(O, NAME)                                                       \
+    case EK_C32: { static KSet s = kset<O, cf32>(NAME "_c32"); return &s; }  \
+    case EK_C64: { static KSet s = kset<O, cf64>(NAME "_c64"); return &s; }
+#define SIGNED_INT(O, NAME)                                                  \
+    case EK_I8:  { static KSet s = kset<O, int8_t>(NAME "_i8"); return &s; } \
+    case EK_U8:  { static KSet s = kset<O, uint8_t>(NAME "_u8"); return &s; } \
+    case EK_I16: { static KSet s = kset<O, int16_t>(NAME "_i16"); return &s; } \
+    case EK_U16: { static KSet s = kset<O, uint16_t>(NAME "_u16"); return &s; } \
+    case EK_I32: { static KSet s = kset<O, int32_t>(NAME "_i32"); return &s; } \
+    case EK_U32: { static KSet s = kset<O, uint32_t>(NAME "_u32"); return &s; } \
+    case EK_I64: { static KSet s = kset<O, int64_t>(NAME "_i64"); return &s; } \
+    case EK_U64: { static KSet s = kset<O, uint64_t>(NAME "_u64"); return &s; }
+#define PAIRS(O, NAME)                                                       \
+    case EK_PFI: { static KSet s = kset<O, pfi>(NAME "_float_int"); return &s; } \
+    case EK_PDI: { static KSet s = kset<O, pdi>(NAME "_double_int"); return &s; } \
+    case EK_PLI: { static KSet s = kset<O, pli>(NAME "_long_int"); return &s; } \
+    case EK_PSI: { static KSet s = kset<O, psi>(NAME "_short_int"); return &s; } \
+    case EK_PII: { static KSet s = kset<O, pii>(NAME "_2int"); return &s; }
+
+// Returns the kernel set, or NULL with *rc set to the reference's answer for
+// that (op, type): 329 where the op's switch has no case for it
+// (global_ops.c:158-161 and every sibling default), MPI_ERR_TYPE where it has
+// one but the type has no device representation (x87 long double), and
+// MPI_ERR_OP for a handle outside MPI_MAX..MPI_MAXLOC.
+static const KSet *lookup(int op, int dtype, int *rc)
+{
+    const int ek = ekind(dtype);
+    *rc = MVX_ERR_OP_NOT_DEFINED;
+    switch (op) {
+    case MPI_MAX:
+        switch (ek) { SIGNED_INT(OMAX, "max") FLOATS(OMAX, "max")
+        case EK_LDBL: *rc = MPI_ERR_TYPE; return nullptr; default: return nullptr; }
+    case MPI_MIN:
+        switch (ek) { SIGNED_INT(OMIN, "min") FLOATS(OMIN, "min")
+        case EK_LDBL: *rc = MPI_ERR_TYPE; return nullptr; default: return nullptr; }
+    case MPI_SUM:
+        switch (ek) { ARITH_INT(OSUM, "sum") FLOATS(OSUM, "sum") CMPLX(OSUM, "sum")
+        case EK_LDBL: *rc = MPI_ERR_TYPE; return nullptr; default: return nullptr; }
+    case MPI_PROD:
+        switch (ek) { ARITH_INT(OPROD, "prod") FLOATS(OPROD, "prod") CMPLX(OPROD, "prod")
+        case EK_LDBL: *rc = MPI_ERR_TYPE; return nullptr; default: return nullptr; }
+    case MPI_LAND:
+        switch (ek) { ARITH_INT(OLAND, "land") FLOATS(OLAND, "land")
+        case EK_LDBL: *rc = MPI_ERR_TYPE; return nullptr; default: return nullptr; }
+    case MPI_LOR:
+        switch (ek) { ARITH_INT(OLOR, "lor") FLOATS(OLOR, "lor")
+        case EK_LDBL: *rc = MPI_ERR_TYPE; return nullptr; default: return nullptr; }
+    case MPI_LXOR:
+        switch (ek) { ARITH_INT(OLXOR, "lxor") FLOATS(OLXOR, "lxor")
+        case EK_LDBL: *rc = MPI_ERR_TYPE; return nullptr; default: return nullptr; }
+    case MPI_BAND:
+        switch (ek) { case EK_BYTE: ARITH_INT(OBAND, "band") default: return nullptr; }
+    case MPI_BOR:
+        switch (ek) { case EK_BYTE: ARITH_INT(OBOR, "bor") default: return nullptr; }
+    case MPI_BXOR:
+        switch (ek) { case EK_BYTE: ARITH_INT(OBXOR, "bxor") default: return nullptr; }
+    case MPI_MAXLOC:
+        switch (ek) { PAIRS(OMAXLOC, "maxloc")
+        case EK_LDBL_INT: *rc = MPI_ERR_TYPE; return nullptr; default: return nullptr; }
+    case MPI_MINLOC:
+        switch (ek) { PAIRS(OMINLOC, "minloc")
+        case EK_LDBL_INT: *rc = MPI_ERR_TYPE; return nullptr; default: return nullptr; }
+    default:
+        *rc = MPI_ERR_OP;
+        return nullptr;
+    }
+}
+
+static int g_block_cap = 2048;  // 256 CUs x 8 resident 256-thread blocks
+static const char *g_last = "";
+
+static int launch(const KSet *ks, const void *fn, int unroll, Params &P,
+                  hipStream_t stream)
+{
+    const int es = ks->esize;
+    const uintptr_t m = (uintptr_t)P.dst & 15;
+    bool same = true;
+    for (int q = 0; q < P.k; ++q) {
+        if (((uintptr_t)P.src[q] & 15) != m) same = false;
+        if (P.fold[q] && ((uintptr_t)P.fold[q] & 15) != m) same = false;
+    }
+    const long pre = (long)((16 - m) & 15);
+    if (same && pre % es == 0) {
+        long head = pre / es;
+        if (head > P.n) head = P.n;
+        P.head = head;
+        P.nvec = (P.n - head) * es / 16;
+        P.vec_ok = 1;
+    } else {
+        P.head = 0;
+        P.nvec = 0;
+        P.vec_ok = 0;
+    }
+    long work = P.vec_ok ? (P.nvec + unroll * 256 - 1) / (unroll * 256)
+                         : (P.n + 255) / 256;
+    if (work < 1) work = 1;
+    const unsigned blocks = (unsigned)(work < g_block_cap ? work : g_block_cap);
+    void *args[] = {&P};
+    hipError_t e = hipLaunchKernel(fn, dim3(blocks), dim3(256), args, 0, stream);
+    g_last = ks->name;
+    return e == hipSuccess ? MPI_SUCCESS : MPI_ERR_OTHER;
+}
+
+}  // namespace mvx
+
+using namespace mvx;
+
+extern "C" int mvx_op_supported(int op, int dtype)
+{
+    int rc;
+    return lookup(op, dtype, &rc) != nullptr;
+}
+
+extern "C" int mvx_dtype_extent(int dtype)
+{
+    const int ek = ekind(dtype);
+    return ek == EK_NONE ? 0 : ek_size(ek);
+}
+
+extern "C" int mvx_op_apply(int op, int dtype, const void *in, void *inout,
+                            size_t n, void *stream)
+{
+    int rc;
+    const KSet *ks = lookup(op, dtype, &rc);
+    if (!ks) return rc;
+    if (n == 0) return MPI_SUCCESS;
+    Params P;
+    memset(&P, 0, sizeof P);
+    P.src[0] = (const char *)inout;   // a: the inout operand
+    P.src[1] = (const char *)in;      // b
+    P.dst = (char *)inout;
+    P.n = (long)n;
+    P.k = 2;
+    return launch(ks, ks->apply, 4, P, (hipStream_t)stream);
+}
+
+extern "C" int mvx_op_combine(int op, int dtype, const void *const *srcs,
+                              const void *const *fold, int k, int shape,
+                              void *dst, size_t n, void *stream)
+{
+    int rc;
+    const KSet *ks = lookup(op, dtype, &rc);
+    if (!ks) return rc;
+    if (k < 1 || k > MVX_COMBINE_KMAX || (shape != MVX_SHAPE_TREE && shape != MVX_SHAPE_CHAIN) || !srcs)
+        return MPI_ERR_ARG;
+    if (n == 0) return MPI_SUCCESS;
+    Params P;
+    memset(&P, 0, sizeof P);
+    for (int q = 0; q < k; ++q) {
+        P.src[q] = (const char *)srcs[q];
+        P.fold[q] = fold ? (const char *)fold[q] : nullptr;
+    }
+    P.dst = (char *)dst;
+    P.n = (long)n;
+    P.k = k;
+    if (k <= 2) return launch(ks, ks->apply, 4, P, (hipStream_t)stream);
+    return launch(ks, shape == MVX_SHAPE_TREE ? ks->tree : ks->chain, 1, P,
+                  (hipStream_t)stream);
+}
+
+extern "C" void mvx_hip_set_launch(int block_cap, int unroll_variant)
+{
+    (void)unroll_variant;
+    g_block_cap = block_cap > 0 ? block_cap : 2048;
+}
+
+extern "C" const char *mvx_hip_last_kernel(void) { return g_last; }

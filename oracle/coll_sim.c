@@ -1,0 +1,577 @@
+/*
+ * coll_sim.c -- TEST INFRASTRUCTURE: lockstep simulation of the reference's
+ * Reduce / Allreduce / Reduce_scatter schedules over p in-memory ranks.
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use
+ * this (via oracle/liboracle.so).  Every message of the reference algorithm
+ * is replayed as a copy from the sender's buffer state at the start of the
+ * round (MPI_Sendrecv pairs are symmetric inside a round), and every (*uop)
+ * call is replayed with the same (in, inout, len) arguments, so combine
+ * order, operand roles and per-rank error codes follow the reference.
+ *
+ *   orc_allreduce       intra_fns_new.c:5453-5790
+ *     self copy 5521, pof2/lgn 5527-5538, non-pof2 fold (even -> rank+1)
+ *     5548-5577, algorithm choice 5589-5591, recursive doubling 5592-5629,
+ *     reduce-scatter by recursive halving 5632-5710, allgather 5712-5754,
+ *     non-pof2 tail 5764-5776, MPIR_Op_errno return 5783-5786.
+ *   orc_reduce          intra_fns_new.c:4519-4989
+ *     Rabenseifner 4619-4874 (odd -> rank-1 fold 4641-4671, halving
+ *     4697-4751, odd-root hand-off 4760-4789, binomial gather 4791-4870);
+ *     binomial tree 4876-4954.
+ *   orc_reduce_scatter  intra_fns_new.c:6191-6503
+ *     recursive halving 6248-6448 (fold 6283-6312, counts 6325-6339,
+ *     mask pof2/2 -> 1 6341-6407), pairwise 6450-6503.
+ * Only predefined (commutative, permanent) ops are simulated.
+ */
+#include <stdlib.h>
+#include <string.h>
+#include "oracle.h"
+
+#define ERR_OP 9
+#define ERR_TYPE 3
+#define ERR_COUNT 2
+
+/* coll_table, intra_fns_new.c:129-132, flattened so that the reference's
+ * lgn = -1 read at p = 1 (row[-1] = previous row's last entry) is kept. */
+static const int coll_table_flat[3 * 5] = {
+    -1, -1, -1, 16384, 16384,
+    -1, 65536, 8192, 4096, 4096,
+    -1, 65536, 4096, 4096, 4096 };
+#define ALLREDUCE_IDX 1
+#define REDUCE_IDX 2
+#define REDSCAT_COMMUTATIVE_LONG_MSG 524288
+
+static int pof2_lgn(int size, int *lgn_out)
+{
+    int pof2 = 1, lgn = -1;
+    while (pof2 <= size) { pof2 <<= 1; lgn++; }
+    pof2 >>= 1;
+    lgn--;
+    if (lgn > 4) lgn = 4;
+    *lgn_out = lgn;
+    return pof2;
+}
+
+/* 32-bit int product as the reference computes count*type_size */
+static int imul32(long a, long b)
+{
+    return (int)(unsigned int)((unsigned long)a * (unsigned long)b);
+}
+
+static int op_valid(int op) { return op >= 100 && op <= 111; }
+
+/* copy n elements, only the bytes in the datatype's type map (MPI message
+ * semantics: padding of the destination is left alone) */
+static void tm_copy(void *dst, const void *src, long n, int dtype)
+{
+    int e, s;
+    long i;
+    orc_dtype_info(dtype, &e, &s);
+    if (e == s) { memcpy(dst, src, (size_t)(n * e)); return; }
+    for (i = 0; i < n; i++) {
+        char *d = (char *)dst + i * e;
+        const char *x = (const char *)src + i * e;
+        switch (dtype) {
+        case 18: case 19: memcpy(d, x, 8); memcpy(d + 8, x + 8, 4); break;
+        case 20: memcpy(d, x, 2); memcpy(d + 4, x + 4, 4); break;
+        default: memcpy(d, x, (size_t)s); break; /* LONG_DOUBLE_INT: v,l */
+        }
+    }
+}
+
+static char *dup_buf(const void *src, long bytes)
+{
+    char *b = (char *)malloc(bytes > 0 ? (size_t)bytes : 1);
+    if (bytes > 0) memcpy(b, src, (size_t)bytes);
+    return b;
+}
+
+static void uop(int op, int dtype, const void *in, void *inout, int len,
+                int *err)
+{
+    int e = orc_op(op, dtype, in, inout, len);
+    if (e) *err = e;
+}
+
+int orc_algorithm(int coll, int p, long total_count, int dtype)
+{
+    int e, ts, lgn, pof2, tv;
+    if (orc_dtype_info(dtype, &e, &ts)) return ORC_ALG_NONE;
+    pof2 = pof2_lgn(p, &lgn);
+    if (coll == ORC_COLL_ALLREDUCE) {
+        if (total_count == 0) return ORC_ALG_NONE;
+        tv = coll_table_flat[ALLREDUCE_IDX * 5 + lgn];
+        if (tv == -1 || imul32(total_count, ts) < tv || total_count < pof2)
+            return ORC_ALG_RECDBL;
+        return ORC_ALG_RABENSEIFNER;
+    }
+    if (coll == ORC_COLL_REDUCE) {
+        if (total_count == 0) return ORC_ALG_NONE;
+        tv = coll_table_flat[REDUCE_IDX * 5 + lgn];
+        if (tv != -1 && imul32(total_count, ts) > tv && total_count >= pof2)
+            return ORC_ALG_RABENSEIFNER;
+        return ORC_ALG_BINOMIAL;
+    }
+    if (coll == ORC_COLL_REDUCE_SCATTER) {
+        if (total_count == 0) return ORC_ALG_NONE;
+        if (imul32(total_count, ts) < REDSCAT_COMMUTATIVE_LONG_MSG)
+            return ORC_ALG_RS_HALVING;
+        return ORC_ALG_RS_PAIRWISE;
+    }
+    return ORC_ALG_NONE;
+}
+
+/* ---------------------------------------------------------------------- */
+
+int orc_allreduce(int p, const void *const *send, void *const *recv,
+                  int count, int dtype, int op, int *rc)
+{
+    int E, TS, r, lgn, pof2, rem, mask, i, alg;
+    int *newrank, *err;
+    char **snap;
+    long bytes;
+
+    if (p <= 0) return 0;
+    if (orc_dtype_info(dtype, &E, &TS)) {
+        for (r = 0; r < p; r++) rc[r] = ERR_TYPE;
+        return 0;
+    }
+    for (r = 0; r < p; r++) rc[r] = 0;
+    if (count < 0) { for (r = 0; r < p; r++) rc[r] = ERR_COUNT; return 0; }
+    if (count == 0) return 0;
+    if (!op_valid(op)) { for (r = 0; r < p; r++) rc[r] = ERR_OP; return 0; }
+
+    bytes = (long)count * E;
+    newrank = (int *)calloc((size_t)p, sizeof(int));
+    err = (int *)calloc((size_t)p, sizeof(int));
+    snap = (char **)calloc((size_t)p, sizeof(char *));
+
+    for (r = 0; r < p; r++) tm_copy(recv[r], send[r], count, dtype);
+    pof2 = pof2_lgn(p, &lgn);
+    rem = p - pof2;
+
+    /* non-pof2 fold: even ranks < 2*rem hand their data to rank+1 */
+    for (r = 0; r < p; r++) {
+        if (r < 2 * rem) {
+            if (r % 2 == 0) newrank[r] = -1;
+            else {
+                char *tmp = dup_buf(recv[r - 1], bytes);
+                uop(op, dtype, tmp, recv[r], count, &err[r]);
+                free(tmp);
+                newrank[r] = r / 2;
+            }
+        } else newrank[r] = r - rem;
+    }
+
+    alg = orc_algorithm(ORC_COLL_ALLREDUCE, p, count, dtype);
+#define REAL(nd) (((nd) < rem) ? (nd) * 2 + 1 : (nd) + rem)
+    if (alg == ORC_ALG_RECDBL) {
+        for (mask = 1; mask < pof2; mask <<= 1) {
+            for (r = 0; r < p; r++)
+                if (newrank[r] != -1) snap[r] = dup_buf(recv[r], bytes);
+            for (r = 0; r < p; r++) {
+                int dst;
+                if (newrank[r] == -1) continue;
+                dst = REAL(newrank[r] ^ mask);
+                uop(op, dtype, snap[dst], recv[r], count, &err[r]);
+            }
+            for (r = 0; r < p; r++) { free(snap[r]); snap[r] = NULL; }
+        }
+    } else {
+        int *cnts = (int *)malloc(sizeof(int) * (size_t)pof2);
+        int *disps = (int *)malloc(sizeof(int) * (size_t)pof2);
+        int *sidx = (int *)calloc((size_t)p, sizeof(int));
+        int *ridx = (int *)calloc((size_t)p, sizeof(int));
+        int *lidx = (int *)calloc((size_t)p, sizeof(int));
+        int *rcnt = (int *)calloc((size_t)p, sizeof(int));
+        for (i = 0; i < pof2 - 1; i++) cnts[i] = count / pof2;
+        cnts[pof2 - 1] = count - (count / pof2) * (pof2 - 1);
+        disps[0] = 0;
+        for (i = 1; i < pof2; i++) disps[i] = disps[i - 1] + cnts[i - 1];
+        for (r = 0; r < p; r++) lidx[r] = pof2;
+
+        /* reduce-scatter, recursive halving with distance 1, 2, 4, ... */
+        for (mask = 1; mask < pof2; mask <<= 1) {
+            for (r = 0; r < p; r++) {
+                int nr = newrank[r], nd;
+                if (nr == -1) continue;
+                nd = nr ^ mask;
+                rcnt[r] = 0;
+                if (nr < nd) {
+                    sidx[r] = ridx[r] + pof2 / (mask * 2);
+                    for (i = ridx[r]; i < sidx[r]; i++) rcnt[r] += cnts[i];
+                } else {
+                    ridx[r] = sidx[r] + pof2 / (mask * 2);
+                    for (i = ridx[r]; i < lidx[r]; i++) rcnt[r] += cnts[i];
+                }
+                snap[r] = dup_buf(recv[r], bytes);
+            }
+            for (r = 0; r < p; r++) {
+                int dst;
+                long off;
+                if (newrank[r] == -1) continue;
+                dst = REAL(newrank[r] ^ mask);
+                off = (long)disps[ridx[r]] * E;
+                uop(op, dtype, snap[dst] + off, (char *)recv[r] + off,
+                    rcnt[r], &err[r]);
+            }
+            for (r = 0; r < p; r++) {
+                free(snap[r]); snap[r] = NULL;
+                if (newrank[r] == -1) continue;
+                sidx[r] = ridx[r];
+                if ((mask << 1) < pof2) lidx[r] = ridx[r] + pof2 / (mask << 1);
+            }
+        }
+        /* allgather by recursive doubling back up */
+        for (mask = pof2 >> 1; mask > 0; mask >>= 1) {
+            for (r = 0; r < p; r++) {
+                int nr = newrank[r], nd;
+                if (nr == -1) continue;
+                nd = nr ^ mask;
+                rcnt[r] = 0;
+                if (nr < nd) {
+                    if (mask != pof2 / 2) lidx[r] = lidx[r] + pof2 / (mask * 2);
+                    ridx[r] = sidx[r] + pof2 / (mask * 2);
+                    for (i = ridx[r]; i < lidx[r]; i++) rcnt[r] += cnts[i];
+                } else {
+                    ridx[r] = sidx[r] - pof2 / (mask * 2);
+                    for (i = ridx[r]; i < sidx[r]; i++) rcnt[r] += cnts[i];
+                }
+                snap[r] = dup_buf(recv[r], bytes);
+            }
+            for (r = 0; r < p; r++) {
+                int dst;
+                long off;
+                if (newrank[r] == -1) continue;
+                dst = REAL(newrank[r] ^ mask);
+                off = (long)disps[ridx[r]] * E;
+                tm_copy((char *)recv[r] + off, snap[dst] + off, rcnt[r], dtype);
+            }
+            for (r = 0; r < p; r++) {
+                free(snap[r]); snap[r] = NULL;
+                if (newrank[r] == -1) continue;
+                if (newrank[r] > (newrank[r] ^ mask)) sidx[r] = ridx[r];
+            }
+        }
+        free(cnts); free(disps); free(sidx); free(ridx); free(lidx);
+        free(rcnt);
+    }
+#undef REAL
+    /* non-pof2 tail: odd ranks < 2*rem return the result to rank-1 */
+    for (r = 0; r < 2 * rem; r += 2) tm_copy(recv[r], recv[r + 1], count, dtype);
+
+    for (r = 0; r < p; r++) rc[r] = err[r];
+    free(newrank); free(err); free(snap);
+    return 0;
+}
+
+/* ---------------------------------------------------------------------- */
+
+int orc_reduce(int p, const void *const *send, void *const *recv,
+               int count, int dtype, int op, int root, int *rc)
+{
+    int E, TS, r, lgn, pof2, rem, mask, i, alg;
+    int *err;
+    char **wb, **snap;
+    long bytes;
+
+    if (p <= 0) return 0;
+    if (orc_dtype_info(dtype, &E, &TS)) {
+        for (r = 0; r < p; r++) rc[r] = ERR_TYPE;
+        return 0;
+    }
+    for (r = 0; r < p; r++) rc[r] = 0;
+    if (count < 0) { for (r = 0; r < p; r++) rc[r] = ERR_COUNT; return 0; }
+    if (count == 0) return 0;
+    if (root < 0 || root >= p) { for (r = 0; r < p; r++) rc[r] = 7; return 0; }
+    if (!op_valid(op)) { for (r = 0; r < p; r++) rc[r] = ERR_OP; return 0; }
+
+    bytes = (long)count * E;
+    err = (int *)calloc((size_t)p, sizeof(int));
+    wb = (char **)calloc((size_t)p, sizeof(char *));
+    snap = (char **)calloc((size_t)p, sizeof(char *));
+    /* non-roots reduce into a private buffer (4590-4594) */
+    for (r = 0; r < p; r++) {
+        wb[r] = (r == root) ? (char *)recv[r] : (char *)calloc((size_t)bytes, 1);
+        tm_copy(wb[r], send[r], count, dtype);
+    }
+    pof2 = pof2_lgn(p, &lgn);
+    alg = orc_algorithm(ORC_COLL_REDUCE, p, count, dtype);
+
+    if (alg == ORC_ALG_RABENSEIFNER) {
+        int *newrank = (int *)calloc((size_t)p, sizeof(int));
+        int *cnts = (int *)malloc(sizeof(int) * (size_t)pof2);
+        int *disps = (int *)malloc(sizeof(int) * (size_t)pof2);
+        int *sidx = (int *)calloc((size_t)p, sizeof(int));
+        int *ridx = (int *)calloc((size_t)p, sizeof(int));
+        int *lidx = (int *)calloc((size_t)p, sizeof(int));
+        int *rcnt = (int *)calloc((size_t)p, sizeof(int));
+        int *active = (int *)calloc((size_t)p, sizeof(int));
+        int *jj = (int *)calloc((size_t)p, sizeof(int));
+        int newroot;
+        rem = p - pof2;
+#define RREAL(nd) (((nd) < rem) ? (nd) * 2 : (nd) + rem)
+        /* fold: odd ranks < 2*rem hand their data to rank-1 */
+        for (r = 0; r < p; r++) {
+            if (r < 2 * rem) {
+                if (r % 2 != 0) newrank[r] = -1;
+                else {
+                    char *tmp = dup_buf(wb[r + 1], bytes);
+                    uop(op, dtype, tmp, wb[r], count, &err[r]);
+                    free(tmp);
+                    newrank[r] = r / 2;
+                }
+            } else newrank[r] = r - rem;
+        }
+        for (i = 0; i < pof2 - 1; i++) cnts[i] = count / pof2;
+        cnts[pof2 - 1] = count - (count / pof2) * (pof2 - 1);
+        disps[0] = 0;
+        for (i = 1; i < pof2; i++) disps[i] = disps[i - 1] + cnts[i - 1];
+        for (r = 0; r < p; r++) lidx[r] = pof2;
+
+        for (mask = 1; mask < pof2; mask <<= 1) {
+            for (r = 0; r < p; r++) {
+                int nr = newrank[r], nd;
+                if (nr == -1) continue;
+                nd = nr ^ mask;
+                rcnt[r] = 0;
+                if (nr < nd) {
+                    sidx[r] = ridx[r] + pof2 / (mask * 2);
+                    for (i = ridx[r]; i < sidx[r]; i++) rcnt[r] += cnts[i];
+                } else {
+                    ridx[r] = sidx[r] + pof2 / (mask * 2);
+                    for (i = ridx[r]; i < lidx[r]; i++) rcnt[r] += cnts[i];
+                }
+                snap[r] = dup_buf(wb[r], bytes);
+            }
+            for (r = 0; r < p; r++) {
+                int dst;
+                long off;
+                if (newrank[r] == -1) continue;
+                dst = RREAL(newrank[r] ^ mask);
+                off = (long)disps[ridx[r]] * E;
+                uop(op, dtype, snap[dst] + off, wb[r] + off, rcnt[r], &err[r]);
+            }
+            for (r = 0; r < p; r++) {
+                free(snap[r]); snap[r] = NULL;
+                if (newrank[r] == -1) continue;
+                sidx[r] = ridx[r];
+                if ((mask << 1) < pof2) lidx[r] = ridx[r] + pof2 / (mask << 1);
+            }
+        }
+
+        /* gather to root */
+        if (root < 2 * rem) {
+            if (root % 2 != 0) {
+                /* root was excluded: newrank 0 (rank 0) hands block 0 over */
+                tm_copy(wb[root], wb[0], cnts[0], dtype);
+                newrank[root] = 0;
+                sidx[root] = 0;
+                lidx[root] = 2;
+                newrank[0] = -1;
+                newroot = 0;
+            } else newroot = root / 2;
+        } else newroot = root - rem;
+
+        {
+            int j0 = 0;
+            mask = 1;
+            while (mask < pof2) { mask <<= 1; j0++; }
+            mask >>= 1;
+            j0--;
+            for (r = 0; r < p; r++) { active[r] = newrank[r] != -1; jj[r] = j0; }
+        }
+        for (; mask > 0; mask >>= 1) {
+            int *sender = (int *)calloc((size_t)p, sizeof(int));
+            int *peer = (int *)calloc((size_t)p, sizeof(int));
+            for (r = 0; r < p; r++) {
+                int nr, nd, dst, ndtr, nrtr;
+                if (!active[r]) continue;
+                nr = newrank[r];
+                nd = nr ^ mask;
+                dst = RREAL(nd);
+                if (nd == 0 && root < 2 * rem && root % 2 != 0) dst = root;
+                ndtr = (nd >> jj[r]) << jj[r];
+                nrtr = (newroot >> jj[r]) << jj[r];
+                rcnt[r] = 0;
+                if (nr < nd) {
+                    if (mask != pof2 / 2) lidx[r] = lidx[r] + pof2 / (mask * 2);
+                    ridx[r] = sidx[r] + pof2 / (mask * 2);
+                    for (i = ridx[r]; i < lidx[r]; i++) rcnt[r] += cnts[i];
+                } else {
+                    ridx[r] = sidx[r] - pof2 / (mask * 2);
+                    for (i = ridx[r]; i < sidx[r]; i++) rcnt[r] += cnts[i];
+                }
+                sender[r] = (ndtr == nrtr);
+                peer[r] = dst;
+            }
+            for (r = 0; r < p; r++)
+                if (active[r]) snap[r] = dup_buf(wb[r], bytes);
+            for (r = 0; r < p; r++) {
+                long off;
+                if (!active[r] || sender[r]) continue;
+                off = (long)disps[ridx[r]] * E;
+                tm_copy(wb[r] + off, snap[peer[r]] + off, rcnt[r], dtype);
+            }
+            for (r = 0; r < p; r++) {
+                free(snap[r]); snap[r] = NULL;
+                if (!active[r]) continue;
+                if (sender[r]) { active[r] = 0; continue; }
+                if (newrank[r] > (newrank[r] ^ mask)) sidx[r] = ridx[r];
+                jj[r]--;
+            }
+            free(sender); free(peer);
+        }
+#undef RREAL
+        free(newrank); free(cnts); free(disps); free(sidx); free(ridx);
+        free(lidx); free(rcnt); free(active); free(jj);
+    } else {
+        /* binomial tree relative to root (commutative: lroot = root) */
+        for (mask = 1; mask < p; mask <<= 1) {
+            int *recv_from = (int *)malloc(sizeof(int) * (size_t)p);
+            for (r = 0; r < p; r++) {
+                int rel = (r - root + p) % p, src;
+                recv_from[r] = -1;
+                /* a rank that already sent has exited: its low bits hold a 1 */
+                if (rel & (mask - 1)) continue;
+                if ((mask & rel) == 0) {
+                    src = rel | mask;
+                    if (src < p) recv_from[r] = (src + root) % p;
+                }
+            }
+            for (r = 0; r < p; r++)
+                if (recv_from[r] >= 0)
+                    snap[recv_from[r]] = dup_buf(wb[recv_from[r]], bytes);
+            for (r = 0; r < p; r++)
+                if (recv_from[r] >= 0)
+                    uop(op, dtype, snap[recv_from[r]], wb[r], count, &err[r]);
+            for (r = 0; r < p; r++) { free(snap[r]); snap[r] = NULL; }
+            free(recv_from);
+        }
+    }
+    for (r = 0; r < p; r++) {
+        rc[r] = err[r];
+        if (r != root) free(wb[r]);
+    }
+    free(err); free(wb); free(snap);
+    return 0;
+}
+
+/* ---------------------------------------------------------------------- */
+
+int orc_reduce_scatter(int p, const void *const *send, void *const *recv,
+                       const int *recvcnts, int dtype, int op, int *rc)
+{
+    int E, TS, r, i, alg, total = 0;
+    int *disps, *err;
+
+    if (p <= 0) return 0;
+    if (orc_dtype_info(dtype, &E, &TS)) {
+        for (r = 0; r < p; r++) rc[r] = ERR_TYPE;
+        return 0;
+    }
+    for (r = 0; r < p; r++) rc[r] = 0;
+    if (!op_valid(op)) { for (r = 0; r < p; r++) rc[r] = ERR_OP; return 0; }
+    disps = (int *)malloc(sizeof(int) * (size_t)p);
+    err = (int *)calloc((size_t)p, sizeof(int));
+    for (i = 0; i < p; i++) { disps[i] = total; total += recvcnts[i]; }
+    if (total == 0) { free(disps); free(err); return 0; }
+
+    alg = orc_algorithm(ORC_COLL_REDUCE_SCATTER, p, total, dtype);
+    if (alg == ORC_ALG_RS_HALVING) {
+        int lgn, pof2 = pof2_lgn(p, &lgn), rem = p - pof2, mask;
+        long bytes = (long)total * E;
+        char **res = (char **)calloc((size_t)p, sizeof(char *));
+        char **snap = (char **)calloc((size_t)p, sizeof(char *));
+        int *newrank = (int *)calloc((size_t)p, sizeof(int));
+        int *newcnts = (int *)malloc(sizeof(int) * (size_t)pof2);
+        int *newdisps = (int *)malloc(sizeof(int) * (size_t)pof2);
+        int *sidx = (int *)calloc((size_t)p, sizeof(int));
+        int *ridx = (int *)calloc((size_t)p, sizeof(int));
+        int *lidx = (int *)calloc((size_t)p, sizeof(int));
+        int *rcnt = (int *)calloc((size_t)p, sizeof(int));
+        for (r = 0; r < p; r++) {
+            res[r] = (char *)calloc((size_t)bytes, 1);
+            tm_copy(res[r], send[r], total, dtype);
+        }
+        for (r = 0; r < p; r++) {
+            if (r < 2 * rem) {
+                if (r % 2 == 0) newrank[r] = -1;
+                else {
+                    char *tmp = dup_buf(res[r - 1], bytes);
+                    uop(op, dtype, tmp, res[r], total, &err[r]);
+                    free(tmp);
+                    newrank[r] = r / 2;
+                }
+            } else newrank[r] = r - rem;
+        }
+        for (i = 0; i < pof2; i++) {
+            int old_i = (i < rem) ? i * 2 + 1 : i + rem;
+            newcnts[i] = (old_i < 2 * rem) ? recvcnts[old_i] + recvcnts[old_i - 1]
+                                           : recvcnts[old_i];
+        }
+        newdisps[0] = 0;
+        for (i = 1; i < pof2; i++) newdisps[i] = newdisps[i - 1] + newcnts[i - 1];
+        for (r = 0; r < p; r++) lidx[r] = pof2;
+
+        for (mask = pof2 >> 1; mask > 0; mask >>= 1) {
+            for (r = 0; r < p; r++) {
+                int nr = newrank[r], nd;
+                if (nr == -1) continue;
+                nd = nr ^ mask;
+                rcnt[r] = 0;
+                if (nr < nd) {
+                    sidx[r] = ridx[r] + mask;
+                    for (i = ridx[r]; i < sidx[r]; i++) rcnt[r] += newcnts[i];
+                } else {
+                    ridx[r] = sidx[r] + mask;
+                    for (i = ridx[r]; i < lidx[r]; i++) rcnt[r] += newcnts[i];
+                }
+                snap[r] = dup_buf(res[r], bytes);
+            }
+            for (r = 0; r < p; r++) {
+                int nd, dst;
+                long off;
+                if (newrank[r] == -1) continue;
+                nd = newrank[r] ^ mask;
+                dst = (nd < rem) ? nd * 2 + 1 : nd + rem;
+                off = (long)newdisps[ridx[r]] * E;
+                if (rcnt[r] != 0)
+                    uop(op, dtype, snap[dst] + off, res[r] + off, rcnt[r], &err[r]);
+            }
+            for (r = 0; r < p; r++) {
+                free(snap[r]); snap[r] = NULL;
+                if (newrank[r] == -1) continue;
+                sidx[r] = ridx[r];
+                lidx[r] = ridx[r] + mask;
+            }
+        }
+        for (r = 0; r < p; r++)
+            if (newrank[r] != -1 && recvcnts[r])
+                tm_copy(recv[r], res[r] + (long)disps[r] * E, recvcnts[r], dtype);
+        for (r = 0; r < 2 * rem; r += 2)
+            if (recvcnts[r])
+                tm_copy(recv[r], res[r + 1] + (long)disps[r] * E, recvcnts[r], dtype);
+        for (r = 0; r < p; r++) free(res[r]);
+        free(res); free(snap); free(newrank); free(newcnts); free(newdisps);
+        free(sidx); free(ridx); free(lidx); free(rcnt);
+    } else {
+        /* pairwise: rank r folds in block r of rank r-1, r-2, ... */
+        for (r = 0; r < p; r++)
+            tm_copy(recv[r], (const char *)send[r] + (long)disps[r] * E,
+                    recvcnts[r], dtype);
+        for (r = 0; r < p; r++) {
+            for (i = 1; i < p; i++) {
+                int src = (r - i + p) % p;
+                long n = recvcnts[r];
+                char *tmp = (char *)calloc((size_t)(n * E + 1), 1);
+                tm_copy(tmp, (const char *)send[src] + (long)disps[r] * E, n, dtype);
+                uop(op, dtype, tmp, recv[r], recvcnts[r], &err[r]);
+                free(tmp);
+            }
+        }
+    }
+    for (r = 0; r < p; r++) rc[r] = err[r];
+    free(disps); free(err);
+    return 0;
+}

@@ -1,0 +1,76 @@
+/*
+ * oracle.h -- CPU restatement of the reference reduction path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and the
+ * cpu_baseline leg of bench.py may load liboracle.so; the product library
+ * (mvapich-cce_amd/) never links or calls it.
+ *
+ * What it restates:
+ *   orc_op()              the 12 predefined MPI_Op kernels,
+ *                         reference src/coll/global_ops.c:56-1745
+ *   orc_allreduce()       intra_Allreduce, src/coll/intra_fns_new.c:5453-5790
+ *   orc_reduce()          intra_Reduce,    src/coll/intra_fns_new.c:4519-4989
+ *   orc_reduce_scatter()  intra_Reduce_scatter (commutative branches),
+ *                         src/coll/intra_fns_new.c:6191-6503
+ * The collectives are simulated with p in-memory ranks stepping in lockstep
+ * through the reference's own send/recv schedule (every round snapshots the
+ * senders before any receiver combines), so the combine order, the operand
+ * roles (which rank's data is `inout`) and the per-rank op error codes are
+ * the reference's, not a derived formula.
+ *
+ * Pinning: the reference cannot be compiled here without its configure step
+ * (global_ops.c needs the generated mpichconf.h), so
+ * this restatement is pinned by the reference's own known-answer tests
+ * (examples/test/coll/ allred.c, redscat.c, coll12.c, redtst.c, shortint.c;
+ * fixtures in tests/golden/) and by the reference
+ * outputs recorded in SURVEY.md Appendix A.3/A.5.
+ */
+#ifndef MVX_ORACLE_H
+#define MVX_ORACLE_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Datatype facts as the reference build registers them (initdte.c:106-280).
+ * Returns 0 and fills extent / type_size (MPI_Type_size: bytes of the type
+ * map, excluding padding), or MPI_ERR_TYPE (3) for an unregistered handle. */
+int orc_dtype_info(int dtype, int *extent, int *type_size);
+
+/* One predefined op: inout[i] = in[i] op inout[i] for i < len.
+ * Returns 0, or 329 (MPIR_ERR_OP_NOT_DEFINED) for an undefined (op, type)
+ * pair (the data is left untouched), or 9 (MPI_ERR_OP) for a bad handle. */
+int orc_op(int op, int dtype, const void *in, void *inout, int len);
+
+/* Collectives over p simulated ranks.  send[r]/recv[r] are rank r's
+ * buffers; rc[r] receives rank r's return code.  Returns 0. */
+int orc_allreduce(int p, const void *const *send, void *const *recv,
+                  int count, int dtype, int op, int *rc);
+int orc_reduce(int p, const void *const *send, void *const *recv,
+               int count, int dtype, int op, int root, int *rc);
+int orc_reduce_scatter(int p, const void *const *send, void *const *recv,
+                       const int *recvcnts, int dtype, int op, int *rc);
+
+/* Which algorithm the reference picks (same thresholds, intra_fns_new.c:
+ * 30-40, 123-132, 4619, 5589, 6248, 6450).  Values: see ORC_ALG_*. */
+#define ORC_ALG_NONE          0
+#define ORC_ALG_RECDBL        1  /* Allreduce recursive doubling          */
+#define ORC_ALG_RABENSEIFNER  2  /* RS (recursive halving) + AG / gather  */
+#define ORC_ALG_BINOMIAL      3  /* Reduce binomial tree                  */
+#define ORC_ALG_RS_HALVING    4  /* Reduce_scatter recursive halving      */
+#define ORC_ALG_RS_PAIRWISE   5  /* Reduce_scatter pairwise exchange      */
+int orc_algorithm(int coll, int p, long total_count, int dtype);
+#define ORC_COLL_ALLREDUCE      1
+#define ORC_COLL_REDUCE         2
+#define ORC_COLL_REDUCE_SCATTER 3
+
+/* Synthetic input generator: xorshift64 seeded
+ * 0x9E3779B97F4A7C15 ^ (rank*1000003 + 1).  dist: 0 mixed-sign f32,
+ * 1 U[0,1) f32, 2 int64 with P(bit)=0.95, 3 FLOAT_INT v=u%1024 l=rank,
+ * 4 FLOAT_INT v=u%1024 l=rank*n+i, 5 raw 64-bit words (any type). */
+void orc_fill(void *buf, long n, int dist, int rank);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

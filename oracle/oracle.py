@@ -1,0 +1,104 @@
+"""TEST INFRASTRUCTURE: ctypes binding of oracle/liboracle.so.
+
+The oracle is the CPU restatement of the reference reduction path
+(oracle/cpu_ops.c restates src/coll/global_ops.c; oracle/coll_sim.c replays
+the src/coll/intra_fns_new.c schedules).  Only tests/, __graft_entry__.smoke()
+and bench.py's cpu_baseline leg import this module; the product package never
+does.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liboracle.so")
+
+ALG_NONE, ALG_RECDBL, ALG_RABENSEIFNER, ALG_BINOMIAL, ALG_RS_HALVING, ALG_RS_PAIRWISE = range(6)
+COLL_ALLREDUCE, COLL_REDUCE, COLL_REDUCE_SCATTER = 1, 2, 3
+
+_lib = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        vp = ctypes.c_void_p
+        L.orc_dtype_info.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
+        L.orc_op.argtypes = [ctypes.c_int, ctypes.c_int, vp, vp, ctypes.c_int]
+        L.orc_allreduce.argtypes = [ctypes.c_int, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.c_int,
+                                    ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
+        L.orc_reduce.argtypes = [ctypes.c_int, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.c_int,
+                                 ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
+        L.orc_reduce_scatter.argtypes = [ctypes.c_int, ctypes.POINTER(vp), ctypes.POINTER(vp),
+                                         ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.c_int,
+                                         ctypes.POINTER(ctypes.c_int)]
+        L.orc_algorithm.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_long, ctypes.c_int]
+        L.orc_fill.argtypes = [vp, ctypes.c_long, ctypes.c_int, ctypes.c_int]
+        L.orc_fill.restype = None
+        _lib = L
+    return _lib
+
+
+def _ptr(a):
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def dtype_info(dtype):
+    e, s = ctypes.c_int(), ctypes.c_int()
+    rc = lib().orc_dtype_info(dtype, ctypes.byref(e), ctypes.byref(s))
+    if rc:
+        raise ValueError("datatype %d not registered" % dtype)
+    return e.value, s.value
+
+
+def op(op_handle, dtype, invec, inoutvec, count):
+    """inoutvec = invec op inoutvec (in place, numpy uint8 views). Returns rc."""
+    return lib().orc_op(op_handle, dtype, _ptr(invec), _ptr(inoutvec), count)
+
+
+def _ptrs(bufs):
+    arr = (ctypes.c_void_p * len(bufs))()
+    for i, b in enumerate(bufs):
+        arr[i] = b.ctypes.data
+    return arr
+
+
+def allreduce(sends, recvs, count, dtype, op_handle):
+    p = len(sends)
+    rc = (ctypes.c_int * p)()
+    lib().orc_allreduce(p, _ptrs(sends), _ptrs(recvs), count, dtype, op_handle, rc)
+    return list(rc)
+
+
+def reduce(sends, recvs, count, dtype, op_handle, root):
+    p = len(sends)
+    rc = (ctypes.c_int * p)()
+    lib().orc_reduce(p, _ptrs(sends), _ptrs(recvs), count, dtype, op_handle, root, rc)
+    return list(rc)
+
+
+def reduce_scatter(sends, recvs, recvcnts, dtype, op_handle):
+    p = len(sends)
+    rc = (ctypes.c_int * p)()
+    cn = (ctypes.c_int * p)(*recvcnts)
+    lib().orc_reduce_scatter(p, _ptrs(sends), _ptrs(recvs), cn, dtype, op_handle, rc)
+    return list(rc)
+
+
+def algorithm(coll, p, total_count, dtype):
+    return lib().orc_algorithm(coll, p, total_count, dtype)
+
+
+def fill(nbytes_or_array, n, dist, rank):
+    a = nbytes_or_array
+    lib().orc_fill(_ptr(a), n, dist, rank)
+    return a

@@ -1,0 +1,69 @@
+"""TEST HELPER: run libmvx.so's per-rank plans on the CPU.
+
+Phase A/C data movement is done with numpy copies (or, in the gloo tests,
+torch.distributed send/recv); phase B's k-leaf combine is evaluated with the
+oracle's op (oracle/cpu_ops.c) in the TREE / CHAIN shape of
+include/mvx_hip.h.  Comparing the result with oracle/coll_sim.c (the
+reference schedule replayed message by message) checks that the plans encode
+the reference's combine order and operand roles exactly.
+"""
+import numpy as np
+
+from oracle import oracle as O
+
+SHAPE_TREE, SHAPE_CHAIN = 0, 1
+
+
+def combine_cpu(op, dtype, esize, leaves, folds, shape, n):
+    """leaves/folds: lists of uint8 arrays (n*esize bytes) or None."""
+    y = []
+    for q, a in enumerate(leaves):
+        v = a.copy()
+        if folds is not None and folds[q] is not None:
+            O.op(op, dtype, folds[q], v, n)
+        y.append(v)
+    k = len(y)
+    if shape == SHAPE_CHAIN:
+        for q in range(1, k):
+            O.op(op, dtype, y[q], y[0], n)
+    else:
+        h = 1
+        while h < k:
+            for q in range(0, k, 2 * h):
+                if q + h < k:
+                    O.op(op, dtype, y[q + h], y[q], n)
+            h *= 2
+    return y[0]
+
+
+def run_plans(plans, sends, recvs):
+    """Execute all ranks' plans.  sends/recvs: per-rank uint8 arrays."""
+    p = len(plans)
+    outs = [None] * p
+    for r, P in enumerate(plans):
+        if not P.has_combine or P.c_cnt == 0:
+            continue
+        E = P.esize
+        lo, hi = P.c_src_off * E, (P.c_src_off + P.c_cnt) * E
+        # phase A: rank r's staging slot s holds sends[s][lo:hi]
+        for s in range(p):
+            if s != r:
+                assert P.a_recv[s].cnt in (0, P.c_cnt), "a_recv must cover the combine range"
+                if P.a_recv[s].cnt:
+                    assert plans[s].a_send[r].cnt == P.a_recv[s].cnt and plans[s].a_send[r].off == P.a_recv[s].off
+        leaves = [sends[P.leaf[q]][lo:hi] for q in range(P.k)]
+        folds = [sends[P.leaf_fold[q]][lo:hi] if P.leaf_fold[q] >= 0 else None for q in range(P.k)]
+        out = combine_cpu(P.op, P.dtype, E, leaves, folds, P.shape, P.c_cnt)
+        outs[r] = out
+        if not P.c_dst_tmp:
+            d = P.c_dst_off * E
+            recvs[r][d:d + out.size] = out
+    # phase C
+    for r, P in enumerate(plans):
+        E = P.esize
+        for d in range(p):
+            if P.b_send[d].cnt:
+                assert plans[d].b_recv[r].cnt == P.b_send[d].cnt and plans[d].b_recv[r].off == P.b_send[d].off
+                o = P.b_send[d].off * E
+                recvs[d][o:o + P.b_send[d].cnt * E] = outs[r][:P.b_send[d].cnt * E]
+    return recvs

@@ -1,0 +1,176 @@
+"""GPU parity: libmvx_hip.so's op / combine kernels against the CPU oracle.
+
+The oracle (oracle/cpu_ops.c) restates src/coll/global_ops.c; every case
+here is bit-exact except NaN payloads of float SUM/PROD results, which the
+reference does not pin either (x86 and gfx950 both return a quiet NaN; the
+payload is compared as "is NaN" -- the 1-ulp-class tolerance of the north
+star, written here as: identical bits, or both NaN).
+"""
+import numpy as np
+import pytest
+
+import mvxtest as T
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("op", T.ALL_OPS)
+@pytest.mark.parametrize("dtype", T.ALL_TYPES)
+def test_op_apply_every_pair(mvx, oracle, op, dtype):
+    """MPIR_<OP> on every datatype: defined pairs bit-exact, undefined -> 329."""
+    n = 4099
+    rc_ref = T.oracle_rc(oracle, op, dtype)
+    a, b = T.rand_vec(dtype, n, 11), T.rand_vec(dtype, n, 12)
+    da, db = T.to_dev(a), T.to_dev(b)
+    rc = mvx.op_apply(op, dtype, da, db, n)
+    if dtype in (mvx.MPI_LONG_DOUBLE, mvx.MPI_LONG_DOUBLE_INT):
+        assert rc in (rc_ref, mvx.MPI_ERR_TYPE)
+        return
+    assert rc == rc_ref, (rc, rc_ref)
+    if rc:
+        assert T.bytes_equal(T.from_dev(db), b), "undefined op must leave inout alone"
+        return
+    ref = b.copy()
+    oracle.op(op, dtype, a.view(np.uint8), ref.view(np.uint8), n)
+    T.assert_same(op, dtype, T.from_dev(db), ref)
+
+
+@pytest.mark.parametrize("dtype", [10, 11, 6, 8, 1, 4, 17, 18, 19, 20, 21, 23, 24])
+@pytest.mark.parametrize("n", [0, 1, 2, 3, 5, 17, 255, 256, 1023, 65537])
+@pytest.mark.parametrize("shift", [(0, 0), (1, 1), (3, 3), (1, 2), (0, 5)])
+def test_op_apply_sizes_and_alignment(mvx, oracle, dtype, n, shift):
+    """Head/tail elements around the 16-byte body, and operands whose
+    alignments differ (scalar path)."""
+    op = mvx.MPI_MAXLOC if dtype in T.PAIRS else mvx.MPI_SUM
+    a, b = T.rand_vec(dtype, n + 8, 21), T.rand_vec(dtype, n + 8, 22)
+    da, db = T.to_dev(a), T.to_dev(b)
+    E = a.dtype.itemsize
+    rc = mvx.op_apply(op, dtype, da.data_ptr() + shift[0] * E, db.data_ptr() + shift[1] * E, n)
+    assert rc == 0
+    ref = b.copy()
+    oracle.op(op, dtype, a[shift[0]:].view(np.uint8), ref[shift[1]:].view(np.uint8), n)
+    T.assert_same(op, dtype, T.from_dev(db), ref)
+
+
+@pytest.mark.parametrize("op,dtype", [(102, 10), (100, 10), (101, 11), (103, 6), (111, 17), (110, 18),
+                                      (105, 8), (108, 4), (102, 24), (103, 23), (111, 20), (110, 21)])
+@pytest.mark.parametrize("k", [1, 2, 3, 4, 5, 6, 7, 8])
+@pytest.mark.parametrize("shape", [0, 1])
+@pytest.mark.parametrize("folded", [False, True])
+def test_combine_tree_chain(mvx, oracle, op, dtype, k, shape, folded):
+    """k-leaf combine (with and without pre-folded leaves) = the same
+    sequence of oracle op calls."""
+    from plan_exec import combine_cpu
+    n = 3001
+    leaves = [T.rand_vec(dtype, n, 100 + q) for q in range(k)]
+    folds = [T.rand_vec(dtype, n, 200 + q) if (folded and q % 2 == 0) else None for q in range(k)]
+    dl = [T.to_dev(x) for x in leaves]
+    dfo = [T.to_dev(x) if x is not None else None for x in folds]
+    dst = T.to_dev(np.zeros_like(leaves[0]))
+    rc = mvx.op_combine(op, dtype, dl, dst, n, shape=shape, folds=dfo)
+    assert rc == 0
+    E = leaves[0].dtype.itemsize
+    ref = combine_cpu(op, dtype, E, [x.view(np.uint8) for x in leaves],
+                      [x.view(np.uint8) if x is not None else None for x in folds], shape, n)
+    T.assert_same(op, dtype, T.from_dev(dst), ref.view(leaves[0].dtype))
+
+
+def test_combine_dst_aliases_leaf0(mvx, oracle):
+    from plan_exec import combine_cpu
+    n = 10007
+    leaves = [T.rand_vec(10, n, q) for q in range(8)]
+    dl = [T.to_dev(x) for x in leaves]
+    rc = mvx.op_combine(102, 10, dl, dl[0], n, shape=0)
+    assert rc == 0
+    ref = combine_cpu(102, 10, 4, [x.view(np.uint8) for x in leaves], None, 0, n)
+    T.assert_same(102, 10, T.from_dev(dl[0]), ref.view(np.float32))
+
+
+def test_combine_bad_args(mvx):
+    import torch
+    x = torch.zeros(16, device="cuda")
+    assert mvx.op_combine(102, 10, [x] * 9, x, 16) == mvx.MPI_ERR_ARG
+    assert mvx.op_combine(102, 10, [x, x], x, 16, shape=7) == mvx.MPI_ERR_ARG
+    assert mvx.op_combine(99, 10, [x, x], x, 16) == mvx.MPI_ERR_OP
+    assert mvx.op_combine(105, 10, [x, x], x, 16) == 329
+
+
+@pytest.mark.parametrize("name,op", [("MPIR_SUM", 102), ("MPIR_MAXF", 100), ("MPIR_MINLOC", 110),
+                                     ("MPIR_BXOR", 109), ("MPIR_LAND", 104)])
+def test_mpir_user_function_symbols(mvx, oracle, name, op):
+    """The predefined ops keep their MPI_User_function ABI (global_ops.c)."""
+    dtype = mvx.MPI_DOUBLE_INT if op == 110 else (mvx.MPI_INT if op == 109 else mvx.MPI_DOUBLE)
+    n = 777
+    a, b = T.rand_vec(dtype, n, 1), T.rand_vec(dtype, n, 2)
+    da, db = T.to_dev(a), T.to_dev(b)
+    mvx.op_errno()
+    mvx.MPIR_call(name, da, db, n, dtype)
+    assert mvx.op_errno() == 0
+    ref = b.copy()
+    oracle.op(op, dtype, a.view(np.uint8), ref.view(np.uint8), n)
+    T.assert_same(op, dtype, T.from_dev(db), ref)
+    # an undefined pair sets the op errno and leaves the data alone
+    mvx.MPIR_call("MPIR_BAND", da, db, n, mvx.MPI_DOUBLE)
+    assert mvx.op_errno() == 329
+
+
+def test_mpir_rejects_host_pointers(mvx):
+    a = np.zeros(64, np.float32)
+    b = np.zeros(64, np.float32)
+    mvx.op_errno()
+    mvx.MPIR_call("MPIR_SUM", a, b, 64, mvx.MPI_FLOAT)
+    assert mvx.op_errno() == mvx.MPI_ERR_BUFFER
+
+
+def test_special_values_float(mvx, oracle):
+    """NaN stickiness of MAX/MIN (coll.h:14-19), signed zeros, infinities,
+    denormals and NaN-vs-value in MAXLOC, elementwise against the oracle."""
+    sp = np.array([np.nan, -np.nan, np.inf, -np.inf, 0.0, -0.0, 1.0, -1.0, 1e-45, -1e-45, 1e-40,
+                   3.4e38, -3.4e38, 1.17549435e-38], np.float32)
+    a = np.repeat(sp, len(sp)).astype(np.float32)
+    b = np.tile(sp, len(sp)).astype(np.float32)
+    n = a.size
+    for op in (100, 101, 102, 103, 104, 106, 108):
+        da, db = T.to_dev(a), T.to_dev(b)
+        assert mvx.op_apply(op, 10, da, db, n) == 0
+        ref = b.copy()
+        oracle.op(op, 10, a.view(np.uint8), ref.view(np.uint8), n)
+        T.assert_same(op, 10, T.from_dev(db), ref)
+    pa = np.zeros(n, mvx.PAIR_FLOAT_INT)
+    pb = np.zeros(n, mvx.PAIR_FLOAT_INT)
+    pa["v"], pb["v"] = a, b
+    pa["l"], pb["l"] = np.arange(n), np.arange(n)[::-1]
+    for op in (110, 111):
+        da, db = T.to_dev(pa), T.to_dev(pb)
+        assert mvx.op_apply(op, 17, da, db, n) == 0
+        ref = pb.copy()
+        oracle.op(op, 17, pa.view(np.uint8), ref.view(np.uint8), n)
+        T.assert_same(op, 17, T.from_dev(db), ref)
+
+
+def test_integer_wrap(mvx, oracle):
+    """Signed overflow wraps exactly as the reference's x86 build."""
+    for dtype, npt in ((6, np.int32), (4, np.int16), (1, np.int8), (8, np.int64)):
+        info = np.iinfo(npt)
+        a = np.array([info.max, info.min, info.max, -1, info.min], npt)
+        b = np.array([1, -1, info.max, info.min, info.min], npt)
+        for op in (102, 103):
+            da, db = T.to_dev(a), T.to_dev(b)
+            assert mvx.op_apply(op, dtype, da, db, a.size) == 0
+            ref = b.copy()
+            oracle.op(op, dtype, a.view(np.uint8), ref.view(np.uint8), a.size)
+            assert np.array_equal(T.from_dev(db), ref)
+
+
+def test_c2_headline_256mib_sum_f32(mvx, oracle):
+    """Config 2 at full size: 256 MiB MPI_SUM on MPI_FLOAT, bit-exact."""
+    n = 64 * 1024 * 1024
+    a = np.empty(n, np.float32)
+    b = np.empty(n, np.float32)
+    oracle.fill(a, n, 0, 0)
+    oracle.fill(b, n, 0, 1)
+    da, db = T.to_dev(a), T.to_dev(b)
+    assert mvx.op_apply(102, 10, da, db, n) == 0
+    oracle.op(102, 10, a.view(np.uint8), b.view(np.uint8), n)
+    got = T.from_dev(db)
+    assert np.array_equal(got.view(np.uint32), b.view(np.uint32))

@@ -1,0 +1,25 @@
+#!/bin/bash
+# One GPU-box session: smoke, GPU parity tests, 1-GPU bench, rocprof trace.
+# Every GPU step has its own time limit; the chain stops at the first failure.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+STAGE=${1:-all}
+run() { echo "== $*" ; "$@"; }
+if [[ $STAGE == all || $STAGE == smoke ]]; then
+  run timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { cat gpurun_out/smoke.log; exit 1; }
+  tail -2 gpurun_out/smoke.log
+fi
+if [[ $STAGE == all || $STAGE == test ]]; then
+  run timeout -k 10 1500 python -m pytest tests -m gpu -x -q -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1 || { tail -60 gpurun_out/pytest_gpu.log; exit 1; }
+  tail -3 gpurun_out/pytest_gpu.log
+fi
+if [[ $STAGE == all || $STAGE == bench ]]; then
+  run timeout -k 10 400 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || { tail -30 gpurun_out/bench.err; exit 1; }
+  cat gpurun_out/bench.json
+fi
+if [[ $STAGE == all || $STAGE == prof ]]; then
+  run timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_kt -o kt -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/prof_kt.log 2>&1 || { tail -30 gpurun_out/prof_kt.log; exit 1; }
+  find gpurun_out/prof_kt -name "*stats*" | head
+fi
