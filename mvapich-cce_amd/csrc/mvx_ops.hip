@@ -40,9 +40,13 @@ enum { OMAX = 0, OMIN, OSUM, OPROD, OLAND, OBAND, OLOR, OBOR, OLXOR, OBXOR,
 struct cf32 { float re, im; };                          // global_ops.c:43-46
 struct cf64 { double re, im; };                         // global_ops.c:48-51
 struct pfi { float v; int32_t l; };                     // initdte.c:74-78
-struct alignas(8) pdi { double v; int32_t l; };         // 16 B, 4 B pad
-struct alignas(8) pli { int64_t v; int32_t l; };        // 16 B, 4 B pad
-struct psi { int16_t v; int32_t l; };                   // 8 B, 2 B pad
+// The padding is an explicit member so the inout operand's padding bytes are
+// carried through the register copy and written back unchanged (an unnamed
+// hole is `undef` to LLVM); the reference never writes them either
+// (global_ops.c:1335-1346 assign value and loc only).
+struct pdi { double v; int32_t l; int32_t pad; };       // 16 B
+struct pli { int64_t v; int32_t l; int32_t pad; };      // 16 B
+struct psi { int16_t v; int16_t pad; int32_t l; };      // 8 B
 struct pii { int32_t v; int32_t l; };                   // MPI_2INT
 static_assert(sizeof(pdi) == 16 && sizeof(pli) == 16 && sizeof(psi) == 8, "");
 

@@ -59,6 +59,12 @@ def _rand_scalar(dt, n, rng):
     return np.where(rng.random(n) < 0.3, small, wide).astype(dt)
 
 
+def clone(a):
+    """Byte-exact copy (ndarray.copy() skips the padding of structured dtypes)."""
+    a = np.ascontiguousarray(a)
+    return a.view(np.uint8).copy().view(a.dtype)
+
+
 def to_dev(a):
     import torch
     return torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).copy()).to("cuda")

@@ -30,7 +30,7 @@ def test_op_apply_every_pair(mvx, oracle, op, dtype):
     if rc:
         assert T.bytes_equal(T.from_dev(db), b), "undefined op must leave inout alone"
         return
-    ref = b.copy()
+    ref = T.clone(b)
     oracle.op(op, dtype, a.view(np.uint8), ref.view(np.uint8), n)
     T.assert_same(op, dtype, T.from_dev(db), ref)
 
@@ -47,7 +47,7 @@ def test_op_apply_sizes_and_alignment(mvx, oracle, dtype, n, shift):
     E = a.dtype.itemsize
     rc = mvx.op_apply(op, dtype, da.data_ptr() + shift[0] * E, db.data_ptr() + shift[1] * E, n)
     assert rc == 0
-    ref = b.copy()
+    ref = T.clone(b)
     oracle.op(op, dtype, a[shift[0]:].view(np.uint8), ref[shift[1]:].view(np.uint8), n)
     T.assert_same(op, dtype, T.from_dev(db), ref)
 
@@ -106,7 +106,7 @@ def test_mpir_user_function_symbols(mvx, oracle, name, op):
     mvx.op_errno()
     mvx.MPIR_call(name, da, db, n, dtype)
     assert mvx.op_errno() == 0
-    ref = b.copy()
+    ref = T.clone(b)
     oracle.op(op, dtype, a.view(np.uint8), ref.view(np.uint8), n)
     T.assert_same(op, dtype, T.from_dev(db), ref)
     # an undefined pair sets the op errno and leaves the data alone
@@ -133,7 +133,7 @@ def test_special_values_float(mvx, oracle):
     for op in (100, 101, 102, 103, 104, 106, 108):
         da, db = T.to_dev(a), T.to_dev(b)
         assert mvx.op_apply(op, 10, da, db, n) == 0
-        ref = b.copy()
+        ref = T.clone(b)
         oracle.op(op, 10, a.view(np.uint8), ref.view(np.uint8), n)
         T.assert_same(op, 10, T.from_dev(db), ref)
     pa = np.zeros(n, mvx.PAIR_FLOAT_INT)
@@ -143,7 +143,7 @@ def test_special_values_float(mvx, oracle):
     for op in (110, 111):
         da, db = T.to_dev(pa), T.to_dev(pb)
         assert mvx.op_apply(op, 17, da, db, n) == 0
-        ref = pb.copy()
+        ref = T.clone(pb)
         oracle.op(op, 17, pa.view(np.uint8), ref.view(np.uint8), n)
         T.assert_same(op, 17, T.from_dev(db), ref)
 
@@ -157,9 +157,9 @@ def test_integer_wrap(mvx, oracle):
         for op in (102, 103):
             da, db = T.to_dev(a), T.to_dev(b)
             assert mvx.op_apply(op, dtype, da, db, a.size) == 0
-            ref = b.copy()
+            ref = T.clone(b)
             oracle.op(op, dtype, a.view(np.uint8), ref.view(np.uint8), a.size)
-            assert np.array_equal(T.from_dev(db), ref)
+            assert T.bytes_equal(T.from_dev(db), ref)
 
 
 def test_c2_headline_256mib_sum_f32(mvx, oracle):
