@@ -36,9 +36,13 @@ def parse():
     ap.add_argument("--mib", type=int, default=256, help="vector size per rank (MiB)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r01_pmc_c2.json"),
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r01", "pmc_c2.json"),
                     help="committed rocprofv3 PMC summary for the traffic field")
     ap.add_argument("--block-cap", type=int, default=0)
+    ap.add_argument("--nt-min-log2", type=int, default=0, help="-1 disables non-temporal loads/stores")
+    ap.add_argument("--sets", type=int, default=4,
+                    help="input sets used round-robin (4 x 512 MiB keeps every step out of the 256 MiB "
+                         "Infinity Cache: the number is HBM-bound, not cache-bound)")
     return ap.parse_args()
 
 
@@ -113,8 +117,8 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     mvx = importlib.import_module("mvapich-cce_amd")
-    if args.block_cap:
-        mvx.set_launch(args.block_cap)
+    if args.block_cap or args.nt_min_log2:
+        mvx.set_launch(args.block_cap, args.nt_min_log2)
 
     nbytes = args.mib * MIB
     n = nbytes // 4
@@ -125,23 +129,29 @@ def main():
         if world > 1:
             dist.barrier()
 
+    it = [0]
     if world == 1:
-        x_in = synth(n, 0, dev)
-        x_io = synth(n, 1, dev)
+        x_in = [synth(n, 2 * s, dev) for s in range(args.sets)]
+        x_io = [synth(n, 2 * s + 1, dev) for s in range(args.sets)]
 
         def step():
-            rc = mvx.op_apply(MPI_SUM, MPI_FLOAT, x_in, x_io, n, stream)
+            s = it[0] % args.sets
+            it[0] += 1
+            rc = mvx.op_apply(MPI_SUM, MPI_FLOAT, x_in[s], x_io[s], n, stream)
             if rc:
                 raise RuntimeError("mvx_op_apply rc=%d" % rc)
         comm = None
     else:
         comm = mvx.Comm.from_torch_distributed(local)
-        sendbuf = synth(n, rank, dev)
-        recvbuf = torch.empty_like(sendbuf)
+        sets = max(1, min(args.sets, 2))
+        sendbuf = [synth(n, rank * 16 + s, dev) for s in range(sets)]
+        recvbuf = [torch.empty_like(sendbuf[0]) for _ in range(sets)]
         comm.reserve(2 * nbytes)
 
         def step():
-            rc = comm.allreduce_async(sendbuf, recvbuf, n, MPI_FLOAT, MPI_SUM, stream)
+            s = it[0] % sets
+            it[0] += 1
+            rc = comm.allreduce_async(sendbuf[s], recvbuf[s], n, MPI_FLOAT, MPI_SUM, stream)
             if rc:
                 raise RuntimeError("mvx_allreduce_async rc=%d" % rc)
 
@@ -176,7 +186,8 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": load_traffic(args.pmc, kernel, nbytes),
                 "kernel": kernel, "kernel_us": round(kern_s * 1e6, 2), "alg_bytes_per_launch": alg_bytes}
-        workload = "config2: device-resident pairwise MPI_SUM float32 %d MiB (local MPI_Op kernel)" % args.mib
+        workload = ("config2: device-resident pairwise MPI_SUM float32 %d MiB (local MPI_Op kernel), "
+                    "%d input sets round-robin" % (args.mib, args.sets))
         par = "single GPU"
     else:
         p = world

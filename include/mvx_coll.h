@@ -59,6 +59,18 @@ int MPI_Op_create(MPI_User_function *function, int commute, MPI_Op *op);
 int MPI_Op_free(MPI_Op *op);
 int MPI_Error_class(int errorcode, int *errorclass);
 
+/* The same three calls under names that cannot collide with a host MPI
+ * library's own MPI_* symbols: what an in-tree binding and
+ * MVX_device_collops call. */
+int mvx_coll_reduce(void *sendbuf, void *recvbuf, int count, MPI_Datatype datatype,
+                    MPI_Op op, int root, MPI_Comm comm);
+int mvx_coll_allreduce(void *sendbuf, void *recvbuf, int count,
+                       MPI_Datatype datatype, MPI_Op op, MPI_Comm comm);
+int mvx_coll_reduce_scatter(void *sendbuf, void *recvbuf, int *recvcnts,
+                            MPI_Datatype datatype, MPI_Op op, MPI_Comm comm);
+/* 1 if p is device (or managed) memory the device path can use directly */
+int mvx_buffer_is_device(const void *p);
+
 int PMPI_Reduce(void *, void *, int, MPI_Datatype, MPI_Op, int, MPI_Comm);
 int PMPI_Allreduce(void *, void *, int, MPI_Datatype, MPI_Op, MPI_Comm);
 int PMPI_Reduce_scatter(void *, void *, int *, MPI_Datatype, MPI_Op, MPI_Comm);

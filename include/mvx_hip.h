@@ -66,8 +66,10 @@ int mvx_op_combine(int op, int dtype, const void *const *srcs,
                    const void *const *fold, int k, int shape, void *dst,
                    size_t n, void *hip_stream);
 
-/* Launch geometry knobs (0 = default), for the tuning sweep in bench.py. */
-void mvx_hip_set_launch(int block_cap, int unroll_variant);
+/* Launch knobs (0 = keep): grid cap in blocks; non-temporal threshold as
+ * log2(bytes touched per launch), -1 = never.  Env: MVX_BLOCK_CAP,
+ * MVX_NT_MIN_BYTES.  Defaults: one-pass grid, non-temporal from 64 MiB. */
+void mvx_hip_set_launch(int block_cap, int nt_min_bytes_log2);
 
 /* Name of the last kernel launched (for profile attribution in bench.py). */
 const char *mvx_hip_last_kernel(void);

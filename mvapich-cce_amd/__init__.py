@@ -99,11 +99,12 @@ def _load():
     c.mvx_comm_reserve.argtypes = [i, sz]
     c.MPI_Comm_size.argtypes = [i, pi]
     c.MPI_Comm_rank.argtypes = [i, pi]
-    for name in ("MPI_Allreduce", "PMPI_Allreduce"):
+    c.mvx_buffer_is_device.argtypes = [vp]
+    for name in ("MPI_Allreduce", "PMPI_Allreduce", "mvx_coll_allreduce"):
         getattr(c, name).argtypes = [vp, vp, i, i, i, i]
-    for name in ("MPI_Reduce", "PMPI_Reduce"):
+    for name in ("MPI_Reduce", "PMPI_Reduce", "mvx_coll_reduce"):
         getattr(c, name).argtypes = [vp, vp, i, i, i, i, i]
-    for name in ("MPI_Reduce_scatter", "PMPI_Reduce_scatter"):
+    for name in ("MPI_Reduce_scatter", "PMPI_Reduce_scatter", "mvx_coll_reduce_scatter"):
         getattr(c, name).argtypes = [vp, vp, pi, i, i, i]
     c.MPI_Op_create.argtypes = [vp, i, pi]
     c.MPI_Op_free.argtypes = [pi]

@@ -57,8 +57,9 @@ def op_combine(op, dtype, srcs, dst, n, shape=0, folds=None, stream=None):
     return hip().mvx_op_combine(op, dtype, _pp(srcs), fo, k, shape, addr(dst), n, stream_handle(stream))
 
 
-def set_launch(block_cap=0, unroll=0):
-    hip().mvx_hip_set_launch(block_cap, unroll)
+def set_launch(block_cap=0, nt_min_log2=0):
+    """Grid cap (blocks) and non-temporal threshold (log2 bytes, -1 = never)."""
+    hip().mvx_hip_set_launch(block_cap, nt_min_log2)
 
 
 def last_kernel():

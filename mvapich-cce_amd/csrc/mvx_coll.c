@@ -415,8 +415,8 @@ static int run(mvx_comm_t *c, const call_t *k, hipStream_t st, int blocking)
 /* ---------------------------------------------------------------------- */
 /* MPI API                                                                */
 
-int MPI_Allreduce(void *sendbuf, void *recvbuf, int count, MPI_Datatype dt,
-                  MPI_Op op, MPI_Comm comm)
+int mvx_coll_allreduce(void *sendbuf, void *recvbuf, int count, MPI_Datatype dt,
+                       MPI_Op op, MPI_Comm comm)
 {
     mvx_comm_t *c = get_comm(comm);
     call_t k;
@@ -431,8 +431,8 @@ int MPI_Allreduce(void *sendbuf, void *recvbuf, int count, MPI_Datatype dt,
     return run(c, &k, c->stream, 1);
 }
 
-int MPI_Reduce(void *sendbuf, void *recvbuf, int count, MPI_Datatype dt,
-               MPI_Op op, int root, MPI_Comm comm)
+int mvx_coll_reduce(void *sendbuf, void *recvbuf, int count, MPI_Datatype dt,
+                    MPI_Op op, int root, MPI_Comm comm)
 {
     mvx_comm_t *c = get_comm(comm);
     call_t k;
@@ -451,8 +451,8 @@ int MPI_Reduce(void *sendbuf, void *recvbuf, int count, MPI_Datatype dt,
     return run(c, &k, c->stream, 1);
 }
 
-int MPI_Reduce_scatter(void *sendbuf, void *recvbuf, int *recvcnts,
-                       MPI_Datatype dt, MPI_Op op, MPI_Comm comm)
+int mvx_coll_reduce_scatter(void *sendbuf, void *recvbuf, int *recvcnts,
+                            MPI_Datatype dt, MPI_Op op, MPI_Comm comm)
 {
     mvx_comm_t *c = get_comm(comm);
     call_t k;
@@ -466,16 +466,25 @@ int MPI_Reduce_scatter(void *sendbuf, void *recvbuf, int *recvcnts,
     return run(c, &k, c->stream, 1);
 }
 
+int MPI_Reduce(void *a, void *b, int n, MPI_Datatype d, MPI_Op o, int r, MPI_Comm c)
+{ return mvx_coll_reduce(a, b, n, d, o, r, c); }
+int MPI_Allreduce(void *a, void *b, int n, MPI_Datatype d, MPI_Op o, MPI_Comm c)
+{ return mvx_coll_allreduce(a, b, n, d, o, c); }
+int MPI_Reduce_scatter(void *a, void *b, int *n, MPI_Datatype d, MPI_Op o, MPI_Comm c)
+{ return mvx_coll_reduce_scatter(a, b, n, d, o, c); }
 int PMPI_Reduce(void *a, void *b, int n, MPI_Datatype d, MPI_Op o, int r, MPI_Comm c)
-{ return MPI_Reduce(a, b, n, d, o, r, c); }
+{ return mvx_coll_reduce(a, b, n, d, o, r, c); }
 int PMPI_Allreduce(void *a, void *b, int n, MPI_Datatype d, MPI_Op o, MPI_Comm c)
-{ return MPI_Allreduce(a, b, n, d, o, c); }
+{ return mvx_coll_allreduce(a, b, n, d, o, c); }
 int PMPI_Reduce_scatter(void *a, void *b, int *n, MPI_Datatype d, MPI_Op o, MPI_Comm c)
-{ return MPI_Reduce_scatter(a, b, n, d, o, c); }
+{ return mvx_coll_reduce_scatter(a, b, n, d, o, c); }
 int PMPI_Op_create(MPI_User_function *f, int cm, MPI_Op *o) { return MPI_Op_create(f, cm, o); }
 int PMPI_Op_free(MPI_Op *o) { return MPI_Op_free(o); }
 
-const mvx_collops MVX_device_collops = { MPI_Reduce, MPI_Allreduce, MPI_Reduce_scatter };
+const mvx_collops MVX_device_collops = { mvx_coll_reduce, mvx_coll_allreduce,
+                                         mvx_coll_reduce_scatter };
+
+int mvx_buffer_is_device(const void *p) { return is_device_ptr(p); }
 
 /* stream-ordered variants: device buffers, no host synchronisation */
 static int async_checks(mvx_comm_t *c, MPI_Datatype dt, MPI_Op op)

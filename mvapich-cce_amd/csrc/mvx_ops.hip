@@ -26,6 +26,8 @@
 // wrap, without UB).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "mvx_mpi.h"
@@ -221,7 +223,25 @@ __device__ __forceinline__ void scalar_elem(const Params &P, long i)
 }
 
 // U = 16-byte chunks per lane per iteration (loads in flight per operand).
-template <int O, typename T, int KMAX, int SHAPE, int U>
+// NT = non-temporal loads and stores (global_load/store_dwordx4 ... nt): for
+// a launch that streams far more than the 256 MiB Infinity Cache, keeping the
+// once-touched lines out of the caches measured 6.59 vs 5.68 TB/s on the
+// config-2 kernel (tools/tune_sum.hip, cold caches).
+template <int NT>
+__device__ __forceinline__ u32x4 ld(const u32x4 *p)
+{
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+
+template <int NT>
+__device__ __forceinline__ void st(u32x4 *p, u32x4 v)
+{
+    if constexpr (NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
+template <int O, typename T, int KMAX, int SHAPE, int U, int NT>
 __global__ void __launch_bounds__(256)
 k_combine(const Params P)
 {
@@ -260,7 +280,7 @@ k_combine(const Params P)
             if (c < P.nvec) {
 #pragma unroll
                 for (int q = 0; q < KMAX; ++q)
-                    if (q < k) x[u][q] = unpack<T>(src[q][c]);
+                    if (q < k) x[u][q] = unpack<T>(ld<NT>(src[q] + c));
             }
         }
 #pragma unroll
@@ -270,7 +290,7 @@ k_combine(const Params P)
                 for (int u = 0; u < U; ++u) {
                     const long c = c0 + (long)u * 256;
                     if (c < P.nvec) {
-                        const Chunk<T> f = unpack<T>(fold[q][c]);
+                        const Chunk<T> f = unpack<T>(ld<NT>(fold[q] + c));
 #pragma unroll
                         for (int j = 0; j < V; ++j) x[u][q].e[j] = F<O, T>::f(x[u][q].e[j], f.e[j]);
                     }
@@ -289,7 +309,7 @@ k_combine(const Params P)
                     reduce_leaves<O, T, KMAX, SHAPE>(y, k);
                     set_fields(x[u][0].e[j], y[0]);  // keeps leaf 0's padding
                 }
-                dst[c] = pack<T>(x[u][0]);
+                st<NT>(dst + c, pack<T>(x[u][0]));
             }
         }
     }
@@ -305,9 +325,9 @@ namespace mvx {
 typedef void (*KFn)(const Params);
 
 struct KSet {
-    const void *apply;  // KMAX 2 (k <= 2), 4 chunks in flight per lane
-    const void *tree;   // KMAX 8, TREE
-    const void *chain;  // KMAX 8, CHAIN
+    const void *apply[2];  // KMAX 2 (k <= 2), 4 chunks in flight per lane; [NT]
+    const void *tree[2];   // KMAX 8, TREE
+    const void *chain[2];  // KMAX 8, CHAIN
     int esize;
     const char *name;
 };
@@ -316,9 +336,12 @@ template <int O, typename T>
 static KSet kset(const char *name)
 {
     KSet s;
-    s.apply = (const void *)&k_combine<O, T, 2, MVX_SHAPE_CHAIN, 4>;
-    s.tree = (const void *)&k_combine<O, T, MVX_COMBINE_KMAX, MVX_SHAPE_TREE, 1>;
-    s.chain = (const void *)&k_combine<O, T, MVX_COMBINE_KMAX, MVX_SHAPE_CHAIN, 1>;
+    s.apply[0] = (const void *)&k_combine<O, T, 2, MVX_SHAPE_CHAIN, 4, 0>;
+    s.apply[1] = (const void *)&k_combine<O, T, 2, MVX_SHAPE_CHAIN, 4, 1>;
+    s.tree[0] = (const void *)&k_combine<O, T, MVX_COMBINE_KMAX, MVX_SHAPE_TREE, 1, 0>;
+    s.tree[1] = (const void *)&k_combine<O, T, MVX_COMBINE_KMAX, MVX_SHAPE_TREE, 1, 1>;
+    s.chain[0] = (const void *)&k_combine<O, T, MVX_COMBINE_KMAX, MVX_SHAPE_CHAIN, 1, 0>;
+    s.chain[1] = (const void *)&k_combine<O, T, MVX_COMBINE_KMAX, MVX_SHAPE_CHAIN, 1, 1>;
     s.esize = (int)sizeof(T);
     s.name = name;
     return s;
@@ -441,12 +464,34 @@ static const KSet *lookup(int op, int dtype, int *rc)
     }
 }
 
-static int g_block_cap = 2048;  // 256 CUs x 8 resident 256-thread blocks
+// Grid: one pass over the data (a block per 256*U chunks) up to this cap,
+// grid-stride beyond it; a full pass measured best on the config-2 kernel.
+static int g_block_cap = 1 << 20;
+// Non-temporal above this many bytes touched by one launch (all operands +
+// the result); below it the result is likely re-read from L2 / MALL.
+static long g_nt_min_bytes = 64L << 20;
 static const char *g_last = "";
+static char g_last_buf[96];
 
-static int launch(const KSet *ks, const void *fn, int unroll, Params &P,
+static void init_env()
+{
+    static int done = 0;
+    if (done) return;
+    done = 1;
+    const char *e = getenv("MVX_NT_MIN_BYTES");
+    if (e) g_nt_min_bytes = atol(e);
+    e = getenv("MVX_BLOCK_CAP");
+    if (e && atoi(e) > 0) g_block_cap = atoi(e);
+}
+
+static int launch(const KSet *ks, const void *const fns[2], int unroll, Params &P,
                   hipStream_t stream)
 {
+    init_env();
+    int nleaves = 0;
+    for (int q = 0; q < P.k; ++q) nleaves += 1 + (P.fold[q] != nullptr);
+    const int nt = (long)(nleaves + 1) * P.n * ks->esize >= g_nt_min_bytes;
+    const void *fn = fns[nt];
     const int es = ks->esize;
     const uintptr_t m = (uintptr_t)P.dst & 15;
     bool same = true;
@@ -472,7 +517,8 @@ static int launch(const KSet *ks, const void *fn, int unroll, Params &P,
     const unsigned blocks = (unsigned)(work < g_block_cap ? work : g_block_cap);
     void *args[] = {&P};
     hipError_t e = hipLaunchKernel(fn, dim3(blocks), dim3(256), args, 0, stream);
-    g_last = ks->name;
+    snprintf(g_last_buf, sizeof g_last_buf, "%s_k%d%s", ks->name, P.k, nt ? "_nt" : "");
+    g_last = g_last_buf;
     return e == hipSuccess ? MPI_SUCCESS : MPI_ERR_OTHER;
 }
 
@@ -533,10 +579,12 @@ extern "C" int mvx_op_combine(int op, int dtype, const void *const *srcs,
                   (hipStream_t)stream);
 }
 
-extern "C" void mvx_hip_set_launch(int block_cap, int unroll_variant)
+extern "C" void mvx_hip_set_launch(int block_cap, int nt_min_bytes_log2)
 {
-    (void)unroll_variant;
-    g_block_cap = block_cap > 0 ? block_cap : 2048;
+    init_env();
+    if (block_cap > 0) g_block_cap = block_cap;
+    if (nt_min_bytes_log2 > 0) g_nt_min_bytes = 1L << nt_min_bytes_log2;
+    if (nt_min_bytes_log2 < 0) g_nt_min_bytes = 1L << 62;   // never non-temporal
 }
 
 extern "C" const char *mvx_hip_last_kernel(void) { return g_last; }

@@ -19,6 +19,12 @@ if [[ $STAGE == all || $STAGE == bench ]]; then
   run timeout -k 10 400 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || { tail -30 gpurun_out/bench.err; exit 1; }
   cat gpurun_out/bench.json
 fi
+if [[ $STAGE == all || $STAGE == pmc ]]; then
+  rm -rf gpurun_out/pmc_fetch gpurun_out/pmc_write
+  run timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o f -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/pmc_fetch.log 2>&1 || { tail -30 gpurun_out/pmc_fetch.log; exit 1; }
+  run timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o w -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/pmc_write.log 2>&1 || { tail -30 gpurun_out/pmc_write.log; exit 1; }
+  python3 tools/pmc_summary.py gpurun_out/pmc_fetch gpurun_out/pmc_write "k_combine<2, float, 2, 1, 4, 1>" sum_f32_k2_nt 268435456 805306368 gpurun_out/pmc_c2.json
+fi
 if [[ $STAGE == all || $STAGE == prof ]]; then
   run timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_kt -o kt -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/prof_kt.log 2>&1 || { tail -30 gpurun_out/prof_kt.log; exit 1; }
   find gpurun_out/prof_kt -name "*stats*" | head
