@@ -282,61 +282,173 @@ static int combine(const mvx_plan *P, const char *const *leafp, void *dst,
                           (size_t)P->c_cnt, st);
 }
 
+/* ---- transports ------------------------------------------------------ */
+/* A phase is a group of point-to-point transfers.  RCCL issues them as one
+ * ncclGroupStart/End; the loopback transport (virtual communicators) records
+ * every rank's sends and receives of a phase and, once all ranks have
+ * issued theirs, pairs them and copies device-to-device.  Both run the same
+ * per-rank phase code below. */
+#define LB_MAX (MVX_MAXP * MVX_MAXP)
+typedef struct { int from, to; const void *src; void *dst; size_t bytes; int used; } lb_msg;
+typedef struct { lb_msg send[LB_MAX], recv[LB_MAX]; int ns, nr; } loopback_t;
+
+typedef struct mvx_xport {
+    int (*start)(struct mvx_xport *);
+    int (*end)(struct mvx_xport *);
+    int (*send)(struct mvx_xport *, const void *, size_t, int, hipStream_t);
+    int (*recv)(struct mvx_xport *, void *, size_t, int, hipStream_t);
+    ncclComm_t nccl;
+    loopback_t *lb;
+    int me;
+} mvx_xport;
+
+static int nc_start(mvx_xport *t) { (void)t; return ncclGroupStart() == ncclSuccess ? 0 : MPI_ERR_OTHER; }
+static int nc_end(mvx_xport *t) { (void)t; return ncclGroupEnd() == ncclSuccess ? 0 : MPI_ERR_OTHER; }
+static int nc_send(mvx_xport *t, const void *b, size_t n, int peer, hipStream_t st)
+{ return ncclSend(b, n, ncclUint8, peer, t->nccl, st) == ncclSuccess ? 0 : MPI_ERR_OTHER; }
+static int nc_recv(mvx_xport *t, void *b, size_t n, int peer, hipStream_t st)
+{ return ncclRecv(b, n, ncclUint8, peer, t->nccl, st) == ncclSuccess ? 0 : MPI_ERR_OTHER; }
+
+static int lb_nop(mvx_xport *t) { (void)t; return 0; }
+static int lb_send(mvx_xport *t, const void *b, size_t n, int peer, hipStream_t st)
+{
+    lb_msg *m;
+    (void)st;
+    if (t->lb->ns >= LB_MAX) return MPI_ERR_INTERN;
+    m = &t->lb->send[t->lb->ns++];
+    m->from = t->me; m->to = peer; m->src = b; m->dst = NULL; m->bytes = n; m->used = 0;
+    return 0;
+}
+static int lb_recv(mvx_xport *t, void *b, size_t n, int peer, hipStream_t st)
+{
+    lb_msg *m;
+    (void)st;
+    if (t->lb->nr >= LB_MAX) return MPI_ERR_INTERN;
+    m = &t->lb->recv[t->lb->nr++];
+    m->from = peer; m->to = t->me; m->src = NULL; m->dst = b; m->bytes = n; m->used = 0;
+    return 0;
+}
+/* pair every receive with its send (same from/to, issue order) and copy */
+static int lb_flush(loopback_t *lb, hipStream_t st)
+{
+    int i, j, rc = MPI_SUCCESS;
+    for (i = 0; i < lb->nr && rc == MPI_SUCCESS; i++) {
+        lb_msg *r = &lb->recv[i];
+        for (j = 0; j < lb->ns; j++) {
+            lb_msg *s = &lb->send[j];
+            if (!s->used && s->from == r->from && s->to == r->to) break;
+        }
+        if (j == lb->ns || lb->send[j].bytes != r->bytes) { rc = MPI_ERR_INTERN; break; }
+        lb->send[j].used = 1;
+        if (hipMemcpyAsync(r->dst, lb->send[j].src, r->bytes, hipMemcpyDeviceToDevice, st) != hipSuccess)
+            rc = MPI_ERR_OTHER;
+    }
+    for (j = 0; j < lb->ns && rc == MPI_SUCCESS; j++)
+        if (!lb->send[j].used) rc = MPI_ERR_INTERN;   /* unmatched send */
+    lb->ns = lb->nr = 0;
+    return rc;
+}
+
+/* ---- one rank's execution of its plan ---------------------------------- */
+typedef struct {
+    const mvx_plan *P;
+    const char *sendbuf;
+    char *recvbuf;
+    char *pool;                     /* this rank's staging region */
+    size_t slot[MVX_MAXP], tmp_off;
+} rank_exec_t;
+
+/* staging layout: one slot per received shard, plus the temporary result
+ * of a non-root Reduce; returns the bytes this rank needs */
+static size_t exec_layout(rank_exec_t *X)
+{
+    const mvx_plan *P = X->P;
+    const long E = P->esize;
+    const char *like = X->sendbuf + P->c_src_off * E;
+    size_t need = 0;
+    int s;
+    for (s = 0; s < P->p; s++) {
+        X->slot[s] = 0;
+        if (P->a_recv[s].cnt) { X->slot[s] = slot_at(need, like); need = X->slot[s] + P->a_recv[s].cnt * E; }
+    }
+    X->tmp_off = 0;
+    if (P->c_dst_tmp) { X->tmp_off = slot_at(need, like); need = X->tmp_off + P->c_cnt * E; }
+    return need;
+}
+
+static char *exec_out(const rank_exec_t *X)
+{
+    const mvx_plan *P = X->P;
+    return P->c_dst_tmp ? X->pool + X->tmp_off : X->recvbuf + P->c_dst_off * P->esize;
+}
+
+/* phase A: shards to the rank that combines them */
+static int exec_phase_a(rank_exec_t *X, mvx_xport *t, hipStream_t st)
+{
+    const mvx_plan *P = X->P;
+    const long E = P->esize;
+    int s, any = 0, rc = 0, rc2;
+    for (s = 0; s < P->p; s++) any |= (P->a_send[s].cnt || P->a_recv[s].cnt);
+    if (!any) return MPI_SUCCESS;
+    if ((rc = t->start(t))) return rc;
+    for (s = 0; s < P->p && !rc; s++) {
+        if (P->a_send[s].cnt)
+            rc = t->send(t, X->sendbuf + P->a_send[s].off * E, (size_t)(P->a_send[s].cnt * E), s, st);
+        if (!rc && P->a_recv[s].cnt)
+            rc = t->recv(t, X->pool + X->slot[s], (size_t)(P->a_recv[s].cnt * E), s, st);
+    }
+    rc2 = t->end(t);
+    return rc ? rc : rc2;
+}
+
+/* phase B: the reference's whole combine tree for this rank's block */
+static int exec_phase_b(rank_exec_t *X, hipStream_t st)
+{
+    const mvx_plan *P = X->P;
+    const long E = P->esize;
+    const char *leafp[MVX_MAXP];
+    int s;
+    if (!P->has_combine || P->c_cnt == 0) return MPI_SUCCESS;
+    for (s = 0; s < P->p; s++)
+        leafp[s] = (s == P->rank) ? X->sendbuf + P->c_src_off * E : X->pool + X->slot[s];
+    return combine(P, leafp, exec_out(X), st);
+}
+
+/* phase C: combined blocks to the ranks that need them */
+static int exec_phase_c(rank_exec_t *X, mvx_xport *t, hipStream_t st)
+{
+    const mvx_plan *P = X->P;
+    const long E = P->esize;
+    int s, any = 0, rc = 0, rc2;
+    for (s = 0; s < P->p; s++) any |= (P->b_send[s].cnt || P->b_recv[s].cnt);
+    if (!any) return MPI_SUCCESS;
+    if ((rc = t->start(t))) return rc;
+    for (s = 0; s < P->p && !rc; s++) {
+        if (P->b_send[s].cnt)
+            rc = t->send(t, exec_out(X), (size_t)(P->b_send[s].cnt * E), s, st);
+        if (!rc && P->b_recv[s].cnt)
+            rc = t->recv(t, X->recvbuf + P->b_recv[s].off * E, (size_t)(P->b_recv[s].cnt * E), s, st);
+    }
+    rc2 = t->end(t);
+    return rc ? rc : rc2;
+}
+
 /* run one rank's plan over RCCL */
 static int exec_plan(mvx_comm_t *c, const mvx_plan *P, const char *sendbuf,
                      char *recvbuf, hipStream_t st)
 {
-    const long E = P->esize;
-    size_t need = 0, slot[MVX_MAXP], tmp_off = 0;
-    const char *like = sendbuf + P->c_src_off * E;
-    const char *leafp[MVX_MAXP];
-    char *out;
-    int s, any, rc;
-
-    for (s = 0; s < P->p; s++) {
-        slot[s] = 0;
-        if (P->a_recv[s].cnt) { slot[s] = slot_at(need, like); need = slot[s] + P->a_recv[s].cnt * E; }
-    }
-    if (P->c_dst_tmp) { tmp_off = slot_at(need, like); need = tmp_off + P->c_cnt * E; }
-    if ((rc = grow(&c->pool, &c->pool_bytes, need))) return rc;
-
-    /* phase A: shards to their combining rank */
-    any = 0;
-    for (s = 0; s < P->p; s++) any |= (P->a_send[s].cnt || P->a_recv[s].cnt);
-    if (any) {
-        NCCL_OK(ncclGroupStart());
-        for (s = 0; s < P->p; s++) {
-            if (P->a_send[s].cnt)
-                NCCL_OK(ncclSend(sendbuf + P->a_send[s].off * E, (size_t)(P->a_send[s].cnt * E),
-                                 ncclUint8, s, c->nccl, st));
-            if (P->a_recv[s].cnt)
-                NCCL_OK(ncclRecv(c->pool + slot[s], (size_t)(P->a_recv[s].cnt * E),
-                                 ncclUint8, s, c->nccl, st));
-        }
-        NCCL_OK(ncclGroupEnd());
-    }
-    /* phase B: the reference's whole combine tree for this rank's block */
-    out = P->c_dst_tmp ? c->pool + tmp_off : recvbuf + P->c_dst_off * E;
-    if (P->has_combine && P->c_cnt > 0) {
-        for (s = 0; s < P->p; s++)
-            leafp[s] = (s == P->rank) ? sendbuf + P->c_src_off * E : c->pool + slot[s];
-        if ((rc = combine(P, leafp, out, st))) return rc;
-    }
-    /* phase C: combined blocks to the ranks that need them */
-    any = 0;
-    for (s = 0; s < P->p; s++) any |= (P->b_send[s].cnt || P->b_recv[s].cnt);
-    if (any) {
-        NCCL_OK(ncclGroupStart());
-        for (s = 0; s < P->p; s++) {
-            if (P->b_send[s].cnt)
-                NCCL_OK(ncclSend(out, (size_t)(P->b_send[s].cnt * E), ncclUint8, s, c->nccl, st));
-            if (P->b_recv[s].cnt)
-                NCCL_OK(ncclRecv(recvbuf + P->b_recv[s].off * E, (size_t)(P->b_recv[s].cnt * E),
-                                 ncclUint8, s, c->nccl, st));
-        }
-        NCCL_OK(ncclGroupEnd());
-    }
-    return MPI_SUCCESS;
+    rank_exec_t X;
+    mvx_xport t;
+    int rc;
+    memset(&t, 0, sizeof t);
+    t.start = nc_start; t.end = nc_end; t.send = nc_send; t.recv = nc_recv;
+    t.nccl = c->nccl; t.me = c->rank;
+    X.P = P; X.sendbuf = sendbuf; X.recvbuf = recvbuf;
+    if ((rc = grow(&c->pool, &c->pool_bytes, exec_layout(&X)))) return rc;
+    X.pool = c->pool;
+    if ((rc = exec_phase_a(&X, &t, st))) return rc;
+    if ((rc = exec_phase_b(&X, st))) return rc;
+    return exec_phase_c(&X, &t, st);
 }
 
 /* ---------------------------------------------------------------------- */
@@ -547,9 +659,12 @@ static int run_multi(mvx_comm_t *c, int coll, void *const *sendbufs,
                      hipStream_t st)
 {
     static mvx_plan plans[MVX_MAXP];
+    static rank_exec_t X[MVX_MAXP];
+    static mvx_xport t[MVX_MAXP];
+    static loopback_t lb;
     const int p = c->size;
-    int r, s, rc, verdict, e, ts;
-    size_t need = 0, tmp_off[MVX_MAXP];
+    int r, rc, verdict, e, ts;
+    size_t need = 0, base[MVX_MAXP];
 
     if (mvx_dtype_info(dt, &e, &ts)) return ERR_TYPE_NULL_CODE;
     for (r = 0; r < p; r++) rcs[r] = 0;
@@ -572,37 +687,28 @@ static int run_multi(mvx_comm_t *c, int coll, void *const *sendbufs,
         if ((nsend && !is_device_ptr(sendbufs[r])) || (nrecv && !is_device_ptr(recvbufs[r])))
             return MPI_ERR_BUFFER;
         if (sendbufs[r] == recvbufs[r]) return MPI_ERR_BUFFER;
-        tmp_off[r] = 0;
-        if (plans[r].c_dst_tmp) {
-            tmp_off[r] = slot_at(need, (const char *)sendbufs[r] + plans[r].c_src_off * e);
-            need = tmp_off[r] + plans[r].c_cnt * e;
-        }
+        X[r].P = &plans[r];
+        X[r].sendbuf = (const char *)sendbufs[r];
+        X[r].recvbuf = (char *)recvbufs[r];
+        base[r] = (need + 255) & ~(size_t)255;
+        need = base[r] + exec_layout(&X[r]);
     }
     if ((rc = grow(&c->pool, &c->pool_bytes, need))) return rc;
-    /* phase A is free: leaves read the other ranks' sendbufs directly */
     for (r = 0; r < p; r++) {
-        const mvx_plan *P = &plans[r];
-        const char *leafp[MVX_MAXP];
-        char *out;
-        if (!P->has_combine || P->c_cnt == 0) continue;
-        for (s = 0; s < p; s++) leafp[s] = (const char *)sendbufs[s] + P->c_src_off * e;
-        out = P->c_dst_tmp ? c->pool + tmp_off[r] : (char *)recvbufs[r] + P->c_dst_off * e;
-        if ((rc = combine(P, leafp, out, st))) return rc;
+        X[r].pool = c->pool + base[r];
+        t[r].start = lb_nop; t[r].end = lb_nop; t[r].send = lb_send; t[r].recv = lb_recv;
+        t[r].lb = &lb; t[r].me = r;
     }
-    /* phase C: device-to-device copies */
-    for (r = 0; r < p; r++) {
-        const mvx_plan *P = &plans[r];
-        const char *out = P->c_dst_tmp ? c->pool + tmp_off[r]
-                                       : (const char *)recvbufs[r] + P->c_dst_off * e;
-        for (s = 0; s < p; s++) {
-            if (!P->b_send[s].cnt) continue;
-            if (hipMemcpyAsync((char *)recvbufs[s] + P->b_send[s].off * e, out,
-                               (size_t)(P->b_send[s].cnt * e), hipMemcpyDeviceToDevice,
-                               st) != hipSuccess)
-                return MPI_ERR_OTHER;
-        }
-    }
-    return MPI_SUCCESS;
+    /* the RCCL path's phase code, every rank in turn, loopback transfers */
+    lb.ns = lb.nr = 0;
+    for (r = 0; r < p; r++)
+        if ((rc = exec_phase_a(&X[r], &t[r], st))) return rc;
+    if ((rc = lb_flush(&lb, st))) return rc;
+    for (r = 0; r < p; r++)
+        if ((rc = exec_phase_b(&X[r], st))) return rc;
+    for (r = 0; r < p; r++)
+        if ((rc = exec_phase_c(&X[r], &t[r], st))) return rc;
+    return lb_flush(&lb, st);
 }
 
 int mvx_allreduce_multi(void *const *sendbufs, void *const *recvbufs, int count,

@@ -1,0 +1,79 @@
+#!/usr/bin/env python3
+"""Per-config combine-kernel throughput on one MI355X (HBM roofline).
+
+For each BASELINE config the device arithmetic is one k-leaf combine over the
+rank's block.  This times exactly that kernel, with the
+shapes the multi-GPU run gives each rank, on rotating buffer sets so that no
+operand is served from the 256 MiB Infinity Cache:
+
+  C2  apply  k=2  SUM   f32         256 MiB vectors        (bench.py's N=1)
+  C3  tree   k=8  SUM   f32         8 x 32 MiB -> 32 MiB   (Allreduce 256 MiB, p=8)
+  C4  chain  k=4  BAND  int64       4 x 256 MiB -> 256 MiB (Reduce_scatter 1 GiB, p=4)
+  C5  tree   k=8  MAXLOC FLOAT_INT  8 x 64 MiB -> 64 MiB   (Allreduce 512 MiB, p=8)
+
+Prints one JSON line per config: algorithmic bytes, kernel time (HIP events on
+the launch stream), GB/s and fraction of the 8 TB/s HBM peak.
+"""
+import importlib
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+MIB = 1 << 20
+PEAK = 8000.0
+
+
+def run(mvx, name, op, dtype, k, shape, leaf_bytes, sets, reps=20, warm=3):
+    import torch
+    n_elems = leaf_bytes // mvx.dtype_info(dtype)[0]
+    bufs = []
+    for s in range(sets):
+        leaves = [torch.randint(0, 1 << 30, (leaf_bytes // 4,), dtype=torch.int32, device="cuda") for _ in range(k)]
+        if dtype == mvx.MPI_FLOAT:
+            leaves = [(x.float() * 1e-6) for x in leaves]
+        dst = torch.empty(leaf_bytes // 4, dtype=torch.int32, device="cuda")
+        bufs.append((leaves, dst))
+    stream = torch.cuda.current_stream()
+
+    def launch(i):
+        leaves, dst = bufs[i % sets]
+        if k == 2 and shape == 1:
+            rc = mvx.op_apply(op, dtype, leaves[1], leaves[0], n_elems, stream)
+        else:
+            rc = mvx.op_combine(op, dtype, leaves, dst, n_elems, shape=shape, stream=stream)
+        assert rc == 0, rc
+
+    for i in range(warm):
+        launch(i)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for i in range(reps):
+        launch(i)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) * 1e3 / reps
+    alg = (k + 1) * leaf_bytes
+    gbs = alg / (us * 1e-6) / 1e9
+    out = {"config": name, "kernel": mvx.last_kernel(), "k": k, "leaf_bytes": leaf_bytes,
+           "alg_bytes_per_launch": alg, "kernel_us": round(us, 2), "achieved_GBps": round(gbs, 1),
+           "hbm_frac": round(gbs / PEAK, 4), "sets": sets}
+    print(json.dumps(out), flush=True)
+    del bufs
+    torch.cuda.empty_cache()
+    return out
+
+
+def main():
+    mvx = importlib.import_module("mvapich-cce_amd")
+    run(mvx, "C2", mvx.MPI_SUM, mvx.MPI_FLOAT, 2, 1, 256 * MIB, 4)
+    run(mvx, "C3", mvx.MPI_SUM, mvx.MPI_FLOAT, 8, 0, 32 * MIB, 4)
+    run(mvx, "C4", mvx.MPI_BAND, mvx.MPI_LONG, 4, 1, 256 * MIB, 2)
+    run(mvx, "C5", mvx.MPI_MAXLOC, mvx.MPI_FLOAT_INT, 8, 0, 64 * MIB, 2)
+
+
+if __name__ == "__main__":
+    main()

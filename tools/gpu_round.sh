@@ -29,3 +29,7 @@ if [[ $STAGE == all || $STAGE == prof ]]; then
   run timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_kt -o kt -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/prof_kt.log 2>&1 || { tail -30 gpurun_out/prof_kt.log; exit 1; }
   find gpurun_out/prof_kt -name "*stats*" | head
 fi
+if [[ $STAGE == all || $STAGE == kernels ]]; then
+  run timeout -k 10 300 python tools/bench_kernels.py > gpurun_out/bench_kernels.jsonl 2> gpurun_out/bench_kernels.err || { tail -20 gpurun_out/bench_kernels.err; exit 1; }
+  cat gpurun_out/bench_kernels.jsonl
+fi
