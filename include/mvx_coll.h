@@ -112,8 +112,9 @@ typedef struct mvx_collops {
 extern const mvx_collops MVX_device_collops;
 
 /* ---- predefined ops as MPI_User_functions (global_ops.c) ---------------
- * invec / inoutvec must be device-accessible; the call completes before it
- * returns.  An undefined (op, type) pair leaves the data alone and sets
+ * invec / inoutvec may be device or host memory (host operands are streamed
+ * through HBM in 32 MiB chunks, H2D / kernel / D2H overlapped); the call
+ * completes before it returns.  An undefined (op, type) pair leaves the data alone and sets
  * mvx_op_errno() to 329, as MPIR_Op_errno (global_ops.c:41). */
 void MPIR_MAXF(void *, void *, int *, MPI_Datatype *);
 void MPIR_MINF(void *, void *, int *, MPI_Datatype *);

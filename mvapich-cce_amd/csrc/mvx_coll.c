@@ -756,16 +756,69 @@ int mvx_op_errno(void)
     return e;
 }
 
+/* Host-resident operands (the reference's MPI user buffers): chunked
+ * pipeline -- H2D of chunk c and its kernel on one stream, D2H of chunk c on
+ * a second stream, so the two PCIe directions and the kernel overlap.
+ * Device operands are used in place. */
+#define HOST_CHUNK_BYTES (32L << 20)
+static char *g_hop_pool;
+static size_t g_hop_bytes;
+static hipStream_t g_hop_s[2];
+static hipEvent_t g_hop_ev;
+
+static int host_apply(MPI_Op op, MPI_Datatype t, const char *in, char *inout, long len,
+                      int in_dev, int io_dev)
+{
+    int e, ts, rc;
+    long chunk, off;
+    size_t bytes;
+    char *din, *dio;
+    mvx_dtype_info(t, &e, &ts);
+    bytes = (size_t)len * e;
+    if (!g_hop_s[0]) {
+        if (hipStreamCreateWithFlags(&g_hop_s[0], hipStreamNonBlocking) != hipSuccess ||
+            hipStreamCreateWithFlags(&g_hop_s[1], hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&g_hop_ev, hipEventDisableTiming) != hipSuccess)
+            return MPI_ERR_OTHER;
+    }
+    if ((rc = grow(&g_hop_pool, &g_hop_bytes, 2 * ((bytes + 255) & ~(size_t)255)))) return rc;
+    din = in_dev ? (char *)in : g_hop_pool;
+    dio = io_dev ? inout : g_hop_pool + ((bytes + 255) & ~(size_t)255);
+    chunk = HOST_CHUNK_BYTES / e;
+    for (off = 0; off < len; off += chunk) {
+        const long n = len - off < chunk ? len - off : chunk;
+        const size_t o = (size_t)off * e, b = (size_t)n * e;
+        if (!in_dev && hipMemcpyAsync(din + o, in + o, b, hipMemcpyHostToDevice, g_hop_s[0]) != hipSuccess)
+            return MPI_ERR_OTHER;
+        if (!io_dev && hipMemcpyAsync(dio + o, inout + o, b, hipMemcpyHostToDevice, g_hop_s[0]) != hipSuccess)
+            return MPI_ERR_OTHER;
+        if ((rc = mvx_op_apply(op, t, din + o, dio + o, (size_t)n, g_hop_s[0]))) return rc;
+        if (!io_dev) {
+            if (hipEventRecord(g_hop_ev, g_hop_s[0]) != hipSuccess ||
+                hipStreamWaitEvent(g_hop_s[1], g_hop_ev, 0) != hipSuccess ||
+                hipMemcpyAsync(inout + o, dio + o, b, hipMemcpyDeviceToHost, g_hop_s[1]) != hipSuccess)
+                return MPI_ERR_OTHER;
+        }
+    }
+    if (hipStreamSynchronize(g_hop_s[0]) != hipSuccess || hipStreamSynchronize(g_hop_s[1]) != hipSuccess)
+        return MPI_ERR_OTHER;
+    return MPI_SUCCESS;
+}
+
 static void uop_call(MPI_Op op, void *in, void *inout, int *len, MPI_Datatype *t)
 {
     int rc;
     if (!len || !t) { g_op_errno = MPI_ERR_ARG; return; }
     rc = mvx_op_apply(op, *t, NULL, NULL, 0, NULL);   /* verdict first */
     if (rc == MPI_SUCCESS && *len > 0) {
-        if (!is_device_ptr(in) || !is_device_ptr(inout)) rc = MPI_ERR_BUFFER;
-        else {
+        const int in_dev = is_device_ptr(in), io_dev = is_device_ptr(inout);
+        if (in_dev && io_dev) {
             rc = mvx_op_apply(op, *t, in, inout, (size_t)*len, NULL);
             if (rc == MPI_SUCCESS && hipStreamSynchronize(NULL) != hipSuccess) rc = MPI_ERR_OTHER;
+        } else if (!in || !inout) {
+            rc = MPI_ERR_BUFFER;
+        } else {
+            rc = host_apply(op, *t, (const char *)in, (char *)inout, *len, in_dev, io_dev);
         }
     }
     if (rc) g_op_errno = rc;

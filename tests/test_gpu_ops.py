@@ -114,12 +114,21 @@ def test_mpir_user_function_symbols(mvx, oracle, name, op):
     assert mvx.op_errno() == 329
 
 
-def test_mpir_rejects_host_pointers(mvx):
-    a = np.zeros(64, np.float32)
-    b = np.zeros(64, np.float32)
+@pytest.mark.parametrize("n", [1, 1000, 9 * 1024 * 1024 + 5])
+@pytest.mark.parametrize("where", ["host-host", "dev-host", "host-dev"])
+def test_mpir_host_buffers(mvx, oracle, n, where):
+    """MPI user buffers live in host memory: the op streams them through HBM
+    (chunked, H2D / kernel / D2H overlapped) with the same device kernel."""
+    a, b = T.rand_vec(10, n, 5), T.rand_vec(10, n, 6)
+    ref = T.clone(b)
+    oracle.op(102, 10, a.view(np.uint8), ref.view(np.uint8), n)
+    ia = T.to_dev(a) if where == "dev-host" else a
+    io = T.to_dev(b) if where == "host-dev" else T.clone(b)
     mvx.op_errno()
-    mvx.MPIR_call("MPIR_SUM", a, b, 64, mvx.MPI_FLOAT)
-    assert mvx.op_errno() == mvx.MPI_ERR_BUFFER
+    mvx.MPIR_call("MPIR_SUM", ia, io, n, mvx.MPI_FLOAT)
+    assert mvx.op_errno() == 0
+    got = T.from_dev(io) if where == "host-dev" else io
+    T.assert_same(102, 10, np.asarray(got).view(np.uint8), ref)
 
 
 def test_special_values_float(mvx, oracle):

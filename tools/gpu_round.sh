@@ -33,3 +33,7 @@ if [[ $STAGE == all || $STAGE == kernels ]]; then
   run timeout -k 10 300 python tools/bench_kernels.py > gpurun_out/bench_kernels.jsonl 2> gpurun_out/bench_kernels.err || { tail -20 gpurun_out/bench_kernels.err; exit 1; }
   cat gpurun_out/bench_kernels.jsonl
 fi
+if [[ $STAGE == all || $STAGE == host ]]; then
+  run timeout -k 10 300 python tools/bench_host.py > gpurun_out/bench_host.jsonl 2> gpurun_out/bench_host.err || { tail -20 gpurun_out/bench_host.err; exit 1; }
+  cat gpurun_out/bench_host.jsonl
+fi
