@@ -55,6 +55,10 @@ int MPI_Allreduce(void *sendbuf, void *recvbuf, int count,
                   MPI_Datatype datatype, MPI_Op op, MPI_Comm comm);
 int MPI_Reduce_scatter(void *sendbuf, void *recvbuf, int *recvcnts,
                        MPI_Datatype datatype, MPI_Op op, MPI_Comm comm);
+/* MPI_Scan (src/coll/scan.c:55-95 -> MPIR_intra_Scan, intra_scan.c:46-150):
+ * inclusive prefix in the reference's recursive-doubling order. */
+int MPI_Scan(void *sendbuf, void *recvbuf, int count, MPI_Datatype datatype,
+             MPI_Op op, MPI_Comm comm);
 int MPI_Op_create(MPI_User_function *function, int commute, MPI_Op *op);
 int MPI_Op_free(MPI_Op *op);
 int MPI_Error_class(int errorcode, int *errorclass);
@@ -68,12 +72,15 @@ int mvx_coll_allreduce(void *sendbuf, void *recvbuf, int count,
                        MPI_Datatype datatype, MPI_Op op, MPI_Comm comm);
 int mvx_coll_reduce_scatter(void *sendbuf, void *recvbuf, int *recvcnts,
                             MPI_Datatype datatype, MPI_Op op, MPI_Comm comm);
+int mvx_coll_scan(void *sendbuf, void *recvbuf, int count, MPI_Datatype datatype,
+                  MPI_Op op, MPI_Comm comm);
 /* 1 if p is device (or managed) memory the device path can use directly */
 int mvx_buffer_is_device(const void *p);
 
 int PMPI_Reduce(void *, void *, int, MPI_Datatype, MPI_Op, int, MPI_Comm);
 int PMPI_Allreduce(void *, void *, int, MPI_Datatype, MPI_Op, MPI_Comm);
 int PMPI_Reduce_scatter(void *, void *, int *, MPI_Datatype, MPI_Op, MPI_Comm);
+int PMPI_Scan(void *, void *, int, MPI_Datatype, MPI_Op, MPI_Comm);
 int PMPI_Op_create(MPI_User_function *, int, MPI_Op *);
 int PMPI_Op_free(MPI_Op *);
 
@@ -84,6 +91,8 @@ int mvx_reduce_async(const void *sendbuf, void *recvbuf, int count,
 int mvx_allreduce_async(const void *sendbuf, void *recvbuf, int count,
                         MPI_Datatype datatype, MPI_Op op, MPI_Comm comm,
                         void *hip_stream);
+int mvx_scan_async(const void *sendbuf, void *recvbuf, int count,
+                   MPI_Datatype datatype, MPI_Op op, MPI_Comm comm, void *hip_stream);
 int mvx_reduce_scatter_async(const void *sendbuf, void *recvbuf,
                              const int *recvcnts, MPI_Datatype datatype,
                              MPI_Op op, MPI_Comm comm, void *hip_stream);
@@ -97,17 +106,21 @@ int mvx_reduce_multi(void *const *sendbufs, void *const *recvbufs, int count,
 int mvx_allreduce_multi(void *const *sendbufs, void *const *recvbufs,
                         int count, MPI_Datatype datatype, MPI_Op op,
                         MPI_Comm comm, int *rc, void *hip_stream);
+int mvx_scan_multi(void *const *sendbufs, void *const *recvbufs, int count,
+                   MPI_Datatype datatype, MPI_Op op, MPI_Comm comm, int *rc,
+                   void *hip_stream);
 int mvx_reduce_scatter_multi(void *const *sendbufs, void *const *recvbufs,
                              const int *recvcnts, MPI_Datatype datatype,
                              MPI_Op op, MPI_Comm comm, int *rc,
                              void *hip_stream);
 
-/* ---- collective function table (mpicoll.h:41-49 members, by handle) ---- */
+/* ---- collective function table (mpicoll.h:41-51 members, by handle) ---- */
 typedef struct mvx_collops {
     int (*Reduce)(void *, void *, int, MPI_Datatype, MPI_Op, int, MPI_Comm);
     int (*Allreduce)(void *, void *, int, MPI_Datatype, MPI_Op, MPI_Comm);
     int (*Reduce_scatter)(void *, void *, int *, MPI_Datatype, MPI_Op,
                           MPI_Comm);
+    int (*Scan)(void *, void *, int, MPI_Datatype, MPI_Op, MPI_Comm);
 } mvx_collops;
 extern const mvx_collops MVX_device_collops;
 
@@ -137,6 +150,7 @@ int mvx_op_errno(void);
 #define MVX_COLL_ALLREDUCE      1
 #define MVX_COLL_REDUCE         2
 #define MVX_COLL_REDUCE_SCATTER 3
+#define MVX_COLL_SCAN           4
 
 #define MVX_ALG_NONE          0
 #define MVX_ALG_RECDBL        1
@@ -144,6 +158,7 @@ int mvx_op_errno(void);
 #define MVX_ALG_BINOMIAL      3
 #define MVX_ALG_RS_HALVING    4
 #define MVX_ALG_RS_PAIRWISE   5
+#define MVX_ALG_SCAN_RECDBL   6
 
 typedef struct { long off, cnt; } mvx_range;   /* in elements */
 
@@ -163,6 +178,7 @@ typedef struct mvx_plan {
     mvx_range a_send[MVX_MAXP];
     mvx_range a_recv[MVX_MAXP];
     int has_combine, k, shape, c_dst_tmp;
+    unsigned tree_mask, chain_mask;   /* the combine program (mvx_hip.h) */
     int leaf[MVX_MAXK];
     int leaf_fold[MVX_MAXK];
     long c_src_off, c_cnt, c_dst_off;

@@ -66,6 +66,21 @@ int mvx_op_combine(int op, int dtype, const void *const *srcs,
                    const void *const *fold, int k, int shape, void *dst,
                    size_t n, void *hip_stream);
 
+/* The general form: leaves as above, then a combine program over them:
+ *   for level l = 0, 1, 2 (h = 2^l), q ascending:
+ *       if tree_mask bit (l*8 + q):  y[q] = op(y[q], y[q+h])
+ *   for q = 1 .. k-1:
+ *       if chain_mask bit q:         y[0] = op(y[0], y[q])
+ *   dst = y[0]
+ * TREE = mvx_tree_mask(k), CHAIN = mvx_chain_mask(k); MPI_Scan's chain of
+ * balanced trees (intra_scan.c:118-147) is a mix.  A step that reaches past
+ * leaf k-1 is MPI_ERR_ARG. */
+int mvx_op_program(int op, int dtype, const void *const *srcs,
+                   const void *const *fold, int k, unsigned tree_mask,
+                   unsigned chain_mask, void *dst, size_t n, void *hip_stream);
+unsigned mvx_tree_mask(int k);
+unsigned mvx_chain_mask(int k);
+
 /* Launch knobs (0 = keep): grid cap in blocks; non-temporal threshold as
  * log2(bytes touched per launch), -1 = never.  Env: MVX_BLOCK_CAP,
  * MVX_NT_MIN_BYTES.  Defaults: one-pass grid, non-temporal from 64 MiB. */

@@ -59,6 +59,7 @@ class Plan(ctypes.Structure):
         ("symmetric", ctypes.c_int), ("calls_uop", ctypes.c_int), ("count", ctypes.c_long),
         ("a_send", Range * MAXP), ("a_recv", Range * MAXP),
         ("has_combine", ctypes.c_int), ("k", ctypes.c_int), ("shape", ctypes.c_int), ("c_dst_tmp", ctypes.c_int),
+        ("tree_mask", ctypes.c_uint), ("chain_mask", ctypes.c_uint),
         ("leaf", ctypes.c_int * MAXK), ("leaf_fold", ctypes.c_int * MAXK),
         ("c_src_off", ctypes.c_long), ("c_cnt", ctypes.c_long), ("c_dst_off", ctypes.c_long),
         ("b_send", Range * MAXP), ("b_recv", Range * MAXP),
@@ -87,6 +88,11 @@ def _load():
     _hip.mvx_dtype_extent.argtypes = [i]
     _hip.mvx_op_apply.argtypes = [i, i, vp, vp, sz, vp]
     _hip.mvx_op_combine.argtypes = [i, i, pvp, pvp, i, i, vp, sz, vp]
+    _hip.mvx_op_program.argtypes = [i, i, pvp, pvp, i, ctypes.c_uint, ctypes.c_uint, vp, sz, vp]
+    _hip.mvx_tree_mask.argtypes = [i]
+    _hip.mvx_tree_mask.restype = ctypes.c_uint
+    _hip.mvx_chain_mask.argtypes = [i]
+    _hip.mvx_chain_mask.restype = ctypes.c_uint
     _hip.mvx_hip_set_launch.argtypes = [i, i]
     _hip.mvx_hip_set_launch.restype = None
     _hip.mvx_hip_last_kernel.restype = ctypes.c_char_p
@@ -104,6 +110,10 @@ def _load():
         getattr(c, name).argtypes = [vp, vp, i, i, i, i]
     for name in ("MPI_Reduce", "PMPI_Reduce", "mvx_coll_reduce"):
         getattr(c, name).argtypes = [vp, vp, i, i, i, i, i]
+    for name in ("MPI_Scan", "PMPI_Scan", "mvx_coll_scan"):
+        getattr(c, name).argtypes = [vp, vp, i, i, i, i]
+    c.mvx_scan_async.argtypes = [vp, vp, i, i, i, i, vp]
+    c.mvx_scan_multi.argtypes = [pvp, pvp, i, i, i, i, pi, vp]
     for name in ("MPI_Reduce_scatter", "PMPI_Reduce_scatter", "mvx_coll_reduce_scatter"):
         getattr(c, name).argtypes = [vp, vp, pi, i, i, i]
     c.MPI_Op_create.argtypes = [vp, i, pi]

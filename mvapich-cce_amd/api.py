@@ -10,8 +10,8 @@ from . import coll, hip
 from .consts import COLL_ALLREDUCE, COLL_REDUCE, COLL_REDUCE_SCATTER  # noqa: F401
 
 __all__ = [
-    "addr", "stream_handle", "op_apply", "op_combine", "Comm",
-    "MPI_Allreduce", "MPI_Reduce", "MPI_Reduce_scatter", "MPI_Op_create", "MPI_Op_free",
+    "addr", "stream_handle", "op_apply", "op_combine", "op_program", "Comm",
+    "MPI_Allreduce", "MPI_Reduce", "MPI_Reduce_scatter", "MPI_Scan", "MPI_Op_create", "MPI_Op_free",
     "MPIR_call", "op_errno", "last_kernel", "set_launch",
 ]
 
@@ -55,6 +55,13 @@ def op_combine(op, dtype, srcs, dst, n, shape=0, folds=None, stream=None):
     k = len(srcs)
     fo = _pp(folds) if folds is not None else None
     return hip().mvx_op_combine(op, dtype, _pp(srcs), fo, k, shape, addr(dst), n, stream_handle(stream))
+
+
+def op_program(op, dtype, srcs, dst, n, tree_mask, chain_mask, folds=None, stream=None):
+    """dst = the combine program (tree steps, then chain) over leaves srcs."""
+    fo = _pp(folds) if folds is not None else None
+    return hip().mvx_op_program(op, dtype, _pp(srcs), fo, len(srcs), tree_mask, chain_mask, addr(dst), n,
+                                stream_handle(stream))
 
 
 def set_launch(block_cap=0, nt_min_log2=0):
@@ -125,6 +132,16 @@ class Comm:
         return coll().mvx_reduce_async(addr(sendbuf), addr(recvbuf), count, dtype, op, root, self.handle,
                                        stream_handle(stream))
 
+    def scan_async(self, sendbuf, recvbuf, count, dtype, op, stream=None):
+        return coll().mvx_scan_async(addr(sendbuf), addr(recvbuf), count, dtype, op, self.handle,
+                                     stream_handle(stream))
+
+    def scan_multi(self, sendbufs, recvbufs, count, dtype, op, stream=None):
+        rc = (ctypes.c_int * self.size)()
+        r = coll().mvx_scan_multi(_pp(sendbufs), _pp(recvbufs), count, dtype, op, self.handle, rc,
+                                  stream_handle(stream))
+        return r, list(rc)
+
     def reduce_scatter_async(self, sendbuf, recvbuf, recvcnts, dtype, op, stream=None):
         cn = (ctypes.c_int * len(recvcnts))(*recvcnts)
         return coll().mvx_reduce_scatter_async(addr(sendbuf), addr(recvbuf), cn, dtype, op, self.handle,
@@ -168,6 +185,10 @@ def MPI_Reduce(sendbuf, recvbuf, count, datatype, op, root, comm):
 def MPI_Reduce_scatter(sendbuf, recvbuf, recvcnts, datatype, op, comm):
     cn = (ctypes.c_int * len(recvcnts))(*recvcnts) if recvcnts is not None else None
     return coll().MPI_Reduce_scatter(addr(sendbuf), addr(recvbuf), cn, datatype, op, _comm_handle(comm))
+
+
+def MPI_Scan(sendbuf, recvbuf, count, datatype, op, comm):
+    return coll().MPI_Scan(addr(sendbuf), addr(recvbuf), count, datatype, op, _comm_handle(comm))
 
 
 _USER_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int),

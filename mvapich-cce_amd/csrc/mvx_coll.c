@@ -278,8 +278,8 @@ static int combine(const mvx_plan *P, const char *const *leafp, void *dst,
         srcs[q] = leafp[P->leaf[q]];
         fold[q] = P->leaf_fold[q] >= 0 ? leafp[P->leaf_fold[q]] : NULL;
     }
-    return mvx_op_combine(P->op, P->dtype, srcs, fold, P->k, P->shape, dst,
-                          (size_t)P->c_cnt, st);
+    return mvx_op_program(P->op, P->dtype, srcs, fold, P->k, P->tree_mask,
+                          P->chain_mask, dst, (size_t)P->c_cnt, st);
 }
 
 /* ---- transports ------------------------------------------------------ */
@@ -494,10 +494,17 @@ static int run(mvx_comm_t *c, const call_t *k, hipStream_t st, int blocking)
     if (rc) return rc;
     if (P.alg == MVX_ALG_NONE) return MPI_SUCCESS;
     verdict = op_verdict(k->op, k->dt);
+    call_sizes(k, c, &nsend, &nrecv);
+    if (verdict == MVX_ERR_OP_NOT_DEFINED && k->coll == MVX_COLL_SCAN) {
+        /* MPIR_intra_Scan ignores MPIR_Op_errno: recvbuf keeps the self copy
+         * (intra_scan.c:100-106) and the call succeeds */
+        if (hipMemcpyAsync(k->recvbuf, k->sendbuf, (size_t)(nsend * e), hipMemcpyDefault, st) != hipSuccess)
+            return MPI_ERR_OTHER;
+        return (blocking && hipStreamSynchronize(st) != hipSuccess) ? MPI_ERR_OTHER : MPI_SUCCESS;
+    }
     if (verdict == MVX_ERR_OP_NOT_DEFINED) return P.calls_uop ? verdict : MPI_SUCCESS;
     if (verdict) return verdict;
 
-    call_sizes(k, c, &nsend, &nrecv);
     sdev = nsend == 0 || is_device_ptr(k->sendbuf);
     rdev = nrecv == 0 || is_device_ptr(k->recvbuf);
     if (sdev && rdev) {
@@ -578,6 +585,26 @@ int mvx_coll_reduce_scatter(void *sendbuf, void *recvbuf, int *recvcnts,
     return run(c, &k, c->stream, 1);
 }
 
+int mvx_coll_scan(void *sendbuf, void *recvbuf, int count, MPI_Datatype dt,
+                  MPI_Op op, MPI_Comm comm)
+{
+    mvx_comm_t *c = get_comm(comm);
+    call_t k;
+    if (!c) return ERR_COMM_NULL_CODE;                       /* scan.c:74-80 */
+    if (mvx_dtype_info(dt, NULL, NULL)) return ERR_TYPE_NULL_CODE;
+    if (sendbuf == recvbuf) return setmsg_code(MPI_ERR_BUFFER, ERR_KIND_ALIAS);
+    if (count < 0) return setmsg_code(MPI_ERR_COUNT, ERR_KIND_DEFAULT);
+    if (count == 0) return MPI_SUCCESS;                     /* scan.c:85 */
+    if (!predefined(op) && !user_op(op)) return MPI_ERR_OP;
+    k.coll = MVX_COLL_SCAN; k.sendbuf = sendbuf; k.recvbuf = recvbuf;
+    k.count = count; k.recvcnts = NULL; k.dt = dt; k.op = op; k.root = 0;
+    return run(c, &k, c->stream, 1);
+}
+
+int MPI_Scan(void *a, void *b, int n, MPI_Datatype d, MPI_Op o, MPI_Comm c)
+{ return mvx_coll_scan(a, b, n, d, o, c); }
+int PMPI_Scan(void *a, void *b, int n, MPI_Datatype d, MPI_Op o, MPI_Comm c)
+{ return mvx_coll_scan(a, b, n, d, o, c); }
 int MPI_Reduce(void *a, void *b, int n, MPI_Datatype d, MPI_Op o, int r, MPI_Comm c)
 { return mvx_coll_reduce(a, b, n, d, o, r, c); }
 int MPI_Allreduce(void *a, void *b, int n, MPI_Datatype d, MPI_Op o, MPI_Comm c)
@@ -594,7 +621,7 @@ int PMPI_Op_create(MPI_User_function *f, int cm, MPI_Op *o) { return MPI_Op_crea
 int PMPI_Op_free(MPI_Op *o) { return MPI_Op_free(o); }
 
 const mvx_collops MVX_device_collops = { mvx_coll_reduce, mvx_coll_allreduce,
-                                         mvx_coll_reduce_scatter };
+                                         mvx_coll_reduce_scatter, mvx_coll_scan };
 
 int mvx_buffer_is_device(const void *p) { return is_device_ptr(p); }
 
@@ -633,6 +660,20 @@ int mvx_reduce_async(const void *sendbuf, void *recvbuf, int count,
     if (sendbuf == recvbuf) return MPI_ERR_BUFFER;
     k.coll = MVX_COLL_REDUCE; k.sendbuf = sendbuf; k.recvbuf = recvbuf;
     k.count = count; k.recvcnts = NULL; k.dt = dt; k.op = op; k.root = root;
+    return run(c, &k, (hipStream_t)stream, 0);
+}
+
+int mvx_scan_async(const void *sendbuf, void *recvbuf, int count,
+                   MPI_Datatype dt, MPI_Op op, MPI_Comm comm, void *stream)
+{
+    mvx_comm_t *c = get_comm(comm);
+    call_t k;
+    int rc = async_checks(c, dt, op);
+    if (rc) return rc;
+    if (count < 0) return MPI_ERR_COUNT;
+    if (sendbuf == recvbuf) return MPI_ERR_BUFFER;
+    k.coll = MVX_COLL_SCAN; k.sendbuf = sendbuf; k.recvbuf = recvbuf;
+    k.count = count; k.recvcnts = NULL; k.dt = dt; k.op = op; k.root = 0;
     return run(c, &k, (hipStream_t)stream, 0);
 }
 
@@ -676,8 +717,12 @@ static int run_multi(mvx_comm_t *c, int coll, void *const *sendbufs,
     if (plans[0].alg == MVX_ALG_NONE) return MPI_SUCCESS;
     verdict = op_verdict(op, dt);
     if (verdict) {
-        for (r = 0; r < p; r++)
+        for (r = 0; r < p; r++) {
             rcs[r] = (verdict == MVX_ERR_OP_NOT_DEFINED && !plans[r].calls_uop) ? 0 : verdict;
+            if (coll == MVX_COLL_SCAN && verdict == MVX_ERR_OP_NOT_DEFINED &&
+                hipMemcpyAsync(recvbufs[r], sendbufs[r], (size_t)(count * e), hipMemcpyDefault, st) != hipSuccess)
+                return MPI_ERR_OTHER;
+        }
         return MPI_SUCCESS;
     }
     for (r = 0; r < p; r++) {
@@ -731,6 +776,16 @@ int mvx_reduce_multi(void *const *sendbufs, void *const *recvbufs, int count,
     if (root < 0 || root >= c->size) return MPI_ERR_ROOT;
     return run_multi(c, MVX_COLL_REDUCE, sendbufs, recvbufs, count, NULL, dt, op,
                      root, rc, (hipStream_t)stream);
+}
+
+int mvx_scan_multi(void *const *sendbufs, void *const *recvbufs, int count,
+                   MPI_Datatype dt, MPI_Op op, MPI_Comm comm, int *rc, void *stream)
+{
+    mvx_comm_t *c = get_comm(comm);
+    if (!c || !c->local) return ERR_COMM_NULL_CODE;
+    if (count < 0) return MPI_ERR_COUNT;
+    return run_multi(c, MVX_COLL_SCAN, sendbufs, recvbufs, count, NULL, dt, op, 0, rc,
+                     (hipStream_t)stream);
 }
 
 int mvx_reduce_scatter_multi(void *const *sendbufs, void *const *recvbufs,

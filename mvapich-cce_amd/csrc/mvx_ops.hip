@@ -6,9 +6,10 @@
 // (src/coll/global_ops.c:56-1745) and every combine order of its collectives
 // (src/coll/intra_fns_new.c): a launch reads k leaf operands (optionally each
 // pre-folded with a partner, the non-power-of-two fold of intra_fns_new.c
-// 5548-5577 / 4641-4671 / 6283-6312), reduces them in registers in a TREE or
-// CHAIN shape whose left operand always plays the reference's `inoutvec`
-// role, and writes the result once.  A k-way combine is one HBM pass instead
+// 5548-5577 / 4641-4671 / 6283-6312), reduces them in registers by a small
+// combine program (tree steps by level, then a chain; include/mvx_hip.h)
+// whose left operand always plays the reference's `inoutvec` role, and
+// writes the result once.  A k-way combine is one HBM pass instead
 // of the reference's log2(p) or p-1 passes over the block.
 //
 // Element-wise: no MFMA, no LDS.  Every lane moves 16 bytes per operand per
@@ -119,22 +120,26 @@ template <typename T> struct F<OBOR, T> {
 template <typename T> struct F<OBXOR, T> {
     static __device__ __forceinline__ T f(T a, T b) { return (T)(a ^ b); }
 };
-// MAXLOC / MINLOC: global_ops.c:1297-1309 and 1524-1536.  Fields are written
-// one by one so the padding bytes of `a` survive (the reference writes only
-// value and loc).
+// MAXLOC / MINLOC: global_ops.c:1297-1309 and 1524-1536, as selects
+// (no divergent branches): equal values keep a's value and the smaller loc;
+// otherwise b wins only if strictly larger (smaller); a NaN on either side
+// compares false both ways, so a is kept.  The padding member comes from a.
+template <typename T, bool MIN>
+__device__ __forceinline__ T loc_op(T a, T b)
+{
+    const bool eq = a.v == b.v;
+    const bool take = MIN ? (a.v > b.v) : (a.v < b.v);
+    const int32_t lmin = (a.l > b.l) ? b.l : a.l;
+    T r = a;
+    r.v = take ? b.v : a.v;
+    r.l = eq ? lmin : (take ? b.l : a.l);
+    return r;
+}
 template <typename T> struct F<OMAXLOC, T> {
-    static __device__ __forceinline__ T f(T a, T b) {
-        if (a.v == b.v) a.l = (a.l > b.l) ? b.l : a.l;
-        else if (a.v < b.v) { a.v = b.v; a.l = b.l; }
-        return a;
-    }
+    static __device__ __forceinline__ T f(T a, T b) { return loc_op<T, false>(a, b); }
 };
 template <typename T> struct F<OMINLOC, T> {
-    static __device__ __forceinline__ T f(T a, T b) {
-        if (a.v == b.v) a.l = (a.l > b.l) ? b.l : a.l;
-        else if (a.v > b.v) { a.v = b.v; a.l = b.l; }
-        return a;
-    }
+    static __device__ __forceinline__ T f(T a, T b) { return loc_op<T, true>(a, b); }
 };
 
 // ---------------------------------------------------------------------------
@@ -149,6 +154,8 @@ struct Params {
     long nvec;   // 16-byte chunks in the body
     int k;       // leaves
     int vec_ok;  // all pointers share their alignment mod 16
+    unsigned tree_mask;   // bit l*8+q: y[q] = op(y[q], y[q + 2^l]), levels 0..2
+    unsigned chain_mask;  // bit q (q >= 1): y[0] = op(y[0], y[q]) after the tree
 };
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));  // one dwordx4
@@ -176,38 +183,34 @@ __device__ __forceinline__ u32x4 pack(const Chunk<T> &c)
     return r;
 }
 
-// write only the value/loc fields of a pair (its padding stays as it was)
-template <typename T>
-__device__ __forceinline__ void set_fields(T &d, const T &r)
-{
-    if constexpr (is_pair<T>::value) { d.v = r.v; d.l = r.l; }
-    else d = r;
-}
-
+// whole-element store: the pair padding is an explicit member carried from
+// leaf 0, so the element path writes the same bytes as the 16-byte path
 template <typename T>
 __device__ __forceinline__ void store_elt(T *d, const T &r) { *d = r; }
-template <> __device__ __forceinline__ void store_elt(pdi *d, const pdi &r) { d->v = r.v; d->l = r.l; }
-template <> __device__ __forceinline__ void store_elt(pli *d, const pli &r) { d->v = r.v; d->l = r.l; }
-template <> __device__ __forceinline__ void store_elt(psi *d, const psi &r) { d->v = r.v; d->l = r.l; }
 
-template <int O, typename T, int KMAX, int SHAPE>
-__device__ __forceinline__ void reduce_leaves(T (&y)[KMAX], int k)
+// The combine program.  KMAX = 2 is the plain op (y0 = y0 op y1); for
+// KMAX = 8 every step is fixed at compile time and switched on by a
+// wave-uniform mask bit, so the leaves stay in registers.
+template <int O, typename T, int KMAX>
+__device__ __forceinline__ void reduce_leaves(T (&y)[KMAX], int k, unsigned tree_mask,
+                                              unsigned chain_mask)
 {
-    if (SHAPE == MVX_SHAPE_CHAIN) {
-#pragma unroll
-        for (int q = 1; q < KMAX; ++q)
-            if (q < k) y[0] = F<O, T>::f(y[0], y[q]);
+    if constexpr (KMAX == 2) {
+        if (k == 2) y[0] = F<O, T>::f(y[0], y[1]);
     } else {
 #pragma unroll
-        for (int h = 1; h < KMAX; h <<= 1) {
+        for (int l = 0; (1 << l) < KMAX; ++l) {
 #pragma unroll
-            for (int q = 0; q + h < KMAX; q += 2 * h)
-                if (q + h < k) y[q] = F<O, T>::f(y[q], y[q + h]);
+            for (int q = 0; q + (1 << l) < KMAX; ++q)
+                if (tree_mask & (1u << (l * 8 + q))) y[q] = F<O, T>::f(y[q], y[q + (1 << l)]);
         }
+#pragma unroll
+        for (int q = 1; q < KMAX; ++q)
+            if (chain_mask & (1u << q)) y[0] = F<O, T>::f(y[0], y[q]);
     }
 }
 
-template <int O, typename T, int KMAX, int SHAPE>
+template <int O, typename T, int KMAX>
 __device__ __forceinline__ void scalar_elem(const Params &P, long i)
 {
     T y[KMAX];
@@ -218,7 +221,7 @@ __device__ __forceinline__ void scalar_elem(const Params &P, long i)
             if (P.fold[q]) y[q] = F<O, T>::f(y[q], reinterpret_cast<const T *>(P.fold[q])[i]);
         }
     }
-    reduce_leaves<O, T, KMAX, SHAPE>(y, P.k);
+    reduce_leaves<O, T, KMAX>(y, P.k, P.tree_mask, P.chain_mask);
     store_elt(reinterpret_cast<T *>(P.dst) + i, y[0]);
 }
 
@@ -241,7 +244,7 @@ __device__ __forceinline__ void st(u32x4 *p, u32x4 v)
     else *p = v;
 }
 
-template <int O, typename T, int KMAX, int SHAPE, int U, int NT>
+template <int O, typename T, int KMAX, int U, int NT>
 __global__ void __launch_bounds__(256)
 k_combine(const Params P)
 {
@@ -250,7 +253,7 @@ k_combine(const Params P)
     const long nthr = (long)gridDim.x * 256;
 
     if (!P.vec_ok) {  // operands misaligned against each other: element loads
-        for (long i = tid; i < P.n; i += nthr) scalar_elem<O, T, KMAX, SHAPE>(P, i);
+        for (long i = tid; i < P.n; i += nthr) scalar_elem<O, T, KMAX>(P, i);
         return;
     }
     {   // head and tail elements outside the aligned body
@@ -258,7 +261,7 @@ k_combine(const Params P)
         const long nscal = P.head + (P.n - tail0);
         for (long s = tid; s < nscal; s += nthr) {
             const long i = s < P.head ? s : tail0 + (s - P.head);
-            scalar_elem<O, T, KMAX, SHAPE>(P, i);
+            scalar_elem<O, T, KMAX>(P, i);
         }
     }
     const u32x4 *src[KMAX];
@@ -270,6 +273,7 @@ k_combine(const Params P)
     }
     u32x4 *dst = reinterpret_cast<u32x4 *>(P.dst + P.head * (long)sizeof(T));
     const int k = P.k;
+    const unsigned tmask = P.tree_mask, cmask = P.chain_mask;
 
     for (long c0 = (long)blockIdx.x * (256 * U) + threadIdx.x; c0 < P.nvec; c0 += nthr * U) {
         Chunk<T> x[U][KMAX];
@@ -297,20 +301,44 @@ k_combine(const Params P)
                 }
             }
         }
+        // the combine program: each wave-uniform step is tested once and
+        // applied to all U*V elements of the batch (chunks past the end
+        // compute on unloaded registers and are never stored)
+        if constexpr (KMAX == 2) {
+            if (k == 2) {
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+#pragma unroll
+                    for (int j = 0; j < V; ++j) x[u][0].e[j] = F<O, T>::f(x[u][0].e[j], x[u][1].e[j]);
+            }
+        } else {
+#pragma unroll
+            for (int l = 0; (1 << l) < KMAX; ++l) {
+#pragma unroll
+                for (int q = 0; q + (1 << l) < KMAX; ++q) {
+                    if (tmask & (1u << (l * 8 + q))) {
+#pragma unroll
+                        for (int u = 0; u < U; ++u)
+#pragma unroll
+                            for (int j = 0; j < V; ++j)
+                                x[u][q].e[j] = F<O, T>::f(x[u][q].e[j], x[u][q + (1 << l)].e[j]);
+                    }
+                }
+            }
+#pragma unroll
+            for (int q = 1; q < KMAX; ++q) {
+                if (cmask & (1u << q)) {
+#pragma unroll
+                    for (int u = 0; u < U; ++u)
+#pragma unroll
+                        for (int j = 0; j < V; ++j) x[u][0].e[j] = F<O, T>::f(x[u][0].e[j], x[u][q].e[j]);
+                }
+            }
+        }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const long c = c0 + (long)u * 256;
-            if (c < P.nvec) {
-#pragma unroll
-                for (int j = 0; j < V; ++j) {
-                    T y[KMAX];
-#pragma unroll
-                    for (int q = 0; q < KMAX; ++q) y[q] = x[u][q].e[j];
-                    reduce_leaves<O, T, KMAX, SHAPE>(y, k);
-                    set_fields(x[u][0].e[j], y[0]);  // keeps leaf 0's padding
-                }
-                st<NT>(dst + c, pack<T>(x[u][0]));
-            }
+            if (c < P.nvec) st<NT>(dst + c, pack<T>(x[u][0]));
         }
     }
 }
@@ -326,8 +354,9 @@ typedef void (*KFn)(const Params);
 
 struct KSet {
     const void *apply[2];  // KMAX 2 (k <= 2), 4 chunks in flight per lane; [NT]
-    const void *tree[2];   // KMAX 8, TREE
-    const void *chain[2];  // KMAX 8, CHAIN
+    const void *prog[2];   // KMAX 8 combine program
+    const void *prog1[2];  // the same with one chunk in flight (A/B knob)
+    int prog_unroll;       // its chunks in flight per lane
     int esize;
     const char *name;
 };
@@ -336,12 +365,16 @@ template <int O, typename T>
 static KSet kset(const char *name)
 {
     KSet s;
-    s.apply[0] = (const void *)&k_combine<O, T, 2, MVX_SHAPE_CHAIN, 4, 0>;
-    s.apply[1] = (const void *)&k_combine<O, T, 2, MVX_SHAPE_CHAIN, 4, 1>;
-    s.tree[0] = (const void *)&k_combine<O, T, MVX_COMBINE_KMAX, MVX_SHAPE_TREE, 1, 0>;
-    s.tree[1] = (const void *)&k_combine<O, T, MVX_COMBINE_KMAX, MVX_SHAPE_TREE, 1, 1>;
-    s.chain[0] = (const void *)&k_combine<O, T, MVX_COMBINE_KMAX, MVX_SHAPE_CHAIN, 1, 0>;
-    s.chain[1] = (const void *)&k_combine<O, T, MVX_COMBINE_KMAX, MVX_SHAPE_CHAIN, 1, 1>;
+    s.apply[0] = (const void *)&k_combine<O, T, 2, 4, 0>;
+    s.apply[1] = (const void *)&k_combine<O, T, 2, 4, 1>;
+    // 1- and 2-byte elements unpack to 16 or 8 values per chunk: one chunk in
+    // flight keeps those programs in registers (two spill to scratch)
+    constexpr int UP = sizeof(T) >= 4 ? 2 : 1;
+    s.prog[0] = (const void *)&k_combine<O, T, MVX_COMBINE_KMAX, UP, 0>;
+    s.prog[1] = (const void *)&k_combine<O, T, MVX_COMBINE_KMAX, UP, 1>;
+    s.prog_unroll = UP;
+    s.prog1[0] = (const void *)&k_combine<O, T, MVX_COMBINE_KMAX, 1, 0>;
+    s.prog1[1] = (const void *)&k_combine<O, T, MVX_COMBINE_KMAX, 1, 1>;
     s.esize = (int)sizeof(T);
     s.name = name;
     return s;
@@ -472,6 +505,7 @@ static int g_block_cap = 1 << 20;
 static long g_nt_min_bytes = 64L << 20;
 static const char *g_last = "";
 static char g_last_buf[96];
+static int g_prog_u1 = 0;   // MVX_PROG_U1=1: program kernels with one chunk in flight
 
 static void init_env()
 {
@@ -480,6 +514,8 @@ static void init_env()
     done = 1;
     const char *e = getenv("MVX_NT_MIN_BYTES");
     if (e) g_nt_min_bytes = atol(e);
+    e = getenv("MVX_PROG_U1");
+    if (e) g_prog_u1 = atoi(e);
     e = getenv("MVX_BLOCK_CAP");
     if (e && atoi(e) > 0) g_block_cap = atoi(e);
 }
@@ -555,15 +591,19 @@ extern "C" int mvx_op_apply(int op, int dtype, const void *in, void *inout,
     return launch(ks, ks->apply, 4, P, (hipStream_t)stream);
 }
 
-extern "C" int mvx_op_combine(int op, int dtype, const void *const *srcs,
-                              const void *const *fold, int k, int shape,
-                              void *dst, size_t n, void *stream)
+extern "C" int mvx_op_program(int op, int dtype, const void *const *srcs,
+                              const void *const *fold, int k, unsigned tree_mask,
+                              unsigned chain_mask, void *dst, size_t n, void *stream)
 {
     int rc;
     const KSet *ks = lookup(op, dtype, &rc);
     if (!ks) return rc;
-    if (k < 1 || k > MVX_COMBINE_KMAX || (shape != MVX_SHAPE_TREE && shape != MVX_SHAPE_CHAIN) || !srcs)
-        return MPI_ERR_ARG;
+    if (k < 1 || k > MVX_COMBINE_KMAX || !srcs) return MPI_ERR_ARG;
+    /* every step must stay inside the k leaves */
+    for (int l = 0; l < 3; ++l)
+        for (int q = 0; q < 8; ++q)
+            if ((tree_mask >> (l * 8 + q) & 1u) && q + (1 << l) >= k) return MPI_ERR_ARG;
+    if ((tree_mask >> 24) || (chain_mask & 1u) || (chain_mask >> k)) return MPI_ERR_ARG;
     if (n == 0) return MPI_SUCCESS;
     Params P;
     memset(&P, 0, sizeof P);
@@ -574,9 +614,41 @@ extern "C" int mvx_op_combine(int op, int dtype, const void *const *srcs,
     P.dst = (char *)dst;
     P.n = (long)n;
     P.k = k;
-    if (k <= 2) return launch(ks, ks->apply, 4, P, (hipStream_t)stream);
-    return launch(ks, shape == MVX_SHAPE_TREE ? ks->tree : ks->chain, 1, P,
-                  (hipStream_t)stream);
+    P.tree_mask = tree_mask;
+    P.chain_mask = chain_mask;
+    if (k <= 2) {
+        /* the only programs over <= 2 leaves: nothing, or y0 op y1 */
+        if (k == 2 && !(tree_mask & 1u) && !(chain_mask & 2u)) return MPI_ERR_ARG;
+        return launch(ks, ks->apply, 4, P, (hipStream_t)stream);
+    }
+    if (g_prog_u1) return launch(ks, ks->prog1, 1, P, (hipStream_t)stream);
+    return launch(ks, ks->prog, ks->prog_unroll, P, (hipStream_t)stream);
+}
+
+extern "C" unsigned mvx_tree_mask(int k)
+{
+    unsigned m = 0;
+    for (int l = 0; (1 << l) < k && l < 3; ++l)
+        for (int q = 0; q + (1 << l) < k; q += 2 << l) m |= 1u << (l * 8 + q);
+    return m;
+}
+
+extern "C" unsigned mvx_chain_mask(int k)
+{
+    return k >= 2 && k <= 32 ? (unsigned)(((1ull << k) - 1) & ~1ull) : 0u;
+}
+
+extern "C" int mvx_op_combine(int op, int dtype, const void *const *srcs,
+                              const void *const *fold, int k, int shape,
+                              void *dst, size_t n, void *stream)
+{
+    if (shape != MVX_SHAPE_TREE && shape != MVX_SHAPE_CHAIN) {
+        int rc;
+        return lookup(op, dtype, &rc) ? MPI_ERR_ARG : rc;
+    }
+    return mvx_op_program(op, dtype, srcs, fold, k,
+                          shape == MVX_SHAPE_TREE ? mvx_tree_mask(k) : 0u,
+                          shape == MVX_SHAPE_CHAIN ? mvx_chain_mask(k) : 0u, dst, n, stream);
 }
 
 extern "C" void mvx_hip_set_launch(int block_cap, int nt_min_bytes_log2)

@@ -121,6 +121,8 @@ int mvx_plan_algorithm(int coll, int p, long total, int dtype)
     case MVX_COLL_REDUCE_SCATTER: /* intra_fns_new.c:6248, 6450 (commutative) */
         return imul32(total, ts) < REDSCAT_COMMUTATIVE_LONG_MSG ? MVX_ALG_RS_HALVING
                                                                 : MVX_ALG_RS_PAIRWISE;
+    case MVX_COLL_SCAN:          /* MPIR_intra_Scan, intra_scan.c:46-150 */
+        return MVX_ALG_SCAN_RECDBL;
     default:
         return MVX_ALG_NONE;
     }
@@ -143,6 +145,21 @@ static int op_symmetric(int op, int dtype)
     default:
         return 0;
     }
+}
+
+/* combine programs (include/mvx_hip.h) */
+static unsigned tree_mask(int k)
+{
+    unsigned m = 0;
+    int l, q;
+    for (l = 0; (1 << l) < k && l < 3; ++l)
+        for (q = 0; q + (1 << l) < k; q += 2 << l) m |= 1u << (l * 8 + q);
+    return m;
+}
+
+static unsigned chain_mask(int k)
+{
+    return k >= 2 ? (unsigned)(((1ull << k) - 1) & ~1ull) : 0u;
 }
 
 static void set_range(mvx_range *r, long off, long cnt)
@@ -209,8 +226,8 @@ static int rs_halving_calls(int p, int rank, const int *recvcnts)
     return 0;
 }
 
-int mvx_plan_build(mvx_plan *P, int coll, int p, int rank, long count,
-                   const int *recvcnts, int dtype, int op, int root)
+static int plan_body(mvx_plan *P, int coll, int p, int rank, long count,
+                     const int *recvcnts, int dtype, int op, int root)
 {
     int e, ts, lgn, pof2, rem, L, i, s, q;
     long cnts[MVX_MAXP], disps[MVX_MAXP];
@@ -323,6 +340,40 @@ int mvx_plan_build(mvx_plan *P, int coll, int p, int rank, long count,
         return MPI_SUCCESS;
     }
 
+    if (coll == MVX_COLL_SCAN) {
+        /* rank r: recv = x_r; for l = 0.. : if bit l of r is set,
+         * recv = op(recv, T(r - 2^l, l)), T(d, l) the partial of d's aligned
+         * 2^l-block, T(d,l) = op(T(d,l-1), T(d^2^(l-1), l-1))
+         * (intra_scan.c:118-147; every member of a block below r exists).
+         * Leaves: [x_r | block l = 0 | block l = 1 | ...] for the set bits,
+         * each block in the tree order x_{dst ^ q}; tree steps inside each
+         * block, then a chain over the block heads. */
+        int pos = 1, l;
+        P->shape = -1;
+        P->calls_uop = 0;          /* MPIR_intra_Scan never reports MPIR_Op_errno */
+        for (s = 0; s < p; s++) {
+            if (s > rank) set_range(&P->a_send[s], 0, count);
+            if (s < rank) set_range(&P->a_recv[s], 0, count);
+        }
+        P->has_combine = 1;
+        P->leaf[0] = rank;
+        P->tree_mask = 0; P->chain_mask = 0;
+        for (l = 0; (1 << l) <= rank; l++) {
+            const int dst = rank ^ (1 << l), size_l = 1 << l;
+            int q, ll;
+            if (!(rank & (1 << l))) continue;
+            for (q = 0; q < size_l; q++) P->leaf[pos + q] = dst ^ q;
+            for (ll = 0; (1 << ll) < size_l; ll++)
+                for (q = 0; q + (1 << ll) < size_l; q += 2 << ll)
+                    P->tree_mask |= 1u << (ll * 8 + pos + q);
+            P->chain_mask |= 1u << pos;
+            pos += size_l;
+        }
+        P->k = pos;                /* = rank + 1 */
+        P->c_src_off = 0; P->c_cnt = count; P->c_dst_off = 0;
+        return MPI_SUCCESS;
+    }
+
     if (coll == MVX_COLL_REDUCE_SCATTER) {
         const long my = recvcnts[rank];
         for (s = 0; s < p; s++) {
@@ -347,4 +398,15 @@ int mvx_plan_build(mvx_plan *P, int coll, int p, int rank, long count,
         return MPI_SUCCESS;
     }
     return MPI_ERR_ARG;
+}
+
+int mvx_plan_build(mvx_plan *P, int coll, int p, int rank, long count,
+                   const int *recvcnts, int dtype, int op, int root)
+{
+    int rc = plan_body(P, coll, p, rank, count, recvcnts, dtype, op, root);
+    if (rc == MPI_SUCCESS && P->has_combine && P->shape >= 0) {
+        P->tree_mask = P->shape == MVX_SHAPE_TREE ? tree_mask(P->k) : 0u;
+        P->chain_mask = P->shape == MVX_SHAPE_CHAIN ? chain_mask(P->k) : 0u;
+    }
+    return rc;
 }

@@ -575,3 +575,46 @@ int orc_reduce_scatter(int p, const void *const *send, void *const *recv,
     free(disps); free(err);
     return 0;
 }
+
+/* ---------------------------------------------------------------------- */
+/* MPIR_intra_Scan, src/coll/intra_scan.c:91-150 (the configured default,
+ * intra_fns_new.c:323-331): recursive doubling over partial scans.  Never
+ * returns MPIR_Op_errno (no check after the loop). */
+int orc_scan(int p, const void *const *send, void *const *recv, int count,
+             int dtype, int op, int *rc)
+{
+    int E, TS, r, mask;
+    char **partial, **snap;
+    long bytes;
+    if (p <= 0) return 0;
+    if (orc_dtype_info(dtype, &E, &TS)) { for (r = 0; r < p; r++) rc[r] = ERR_TYPE; return 0; }
+    for (r = 0; r < p; r++) rc[r] = 0;
+    if (count < 0) { for (r = 0; r < p; r++) rc[r] = ERR_COUNT; return 0; }
+    if (count == 0) return 0;
+    if (!op_valid(op)) { for (r = 0; r < p; r++) rc[r] = ERR_OP; return 0; }
+    bytes = (long)count * E;
+    partial = (char **)calloc((size_t)p, sizeof(char *));
+    snap = (char **)calloc((size_t)p, sizeof(char *));
+    for (r = 0; r < p; r++) {
+        tm_copy(recv[r], send[r], count, dtype);
+        partial[r] = (char *)calloc((size_t)bytes, 1);
+        tm_copy(partial[r], send[r], count, dtype);
+    }
+    for (mask = 1; mask < p; mask <<= 1) {
+        for (r = 0; r < p; r++) snap[r] = dup_buf(partial[r], bytes);
+        for (r = 0; r < p; r++) {
+            int dst = r ^ mask, dummy = 0;
+            if (dst >= p) continue;
+            if (r > dst) {
+                uop(op, dtype, snap[dst], partial[r], count, &dummy);
+                uop(op, dtype, snap[dst], recv[r], count, &dummy);
+            } else {
+                uop(op, dtype, snap[dst], partial[r], count, &dummy);
+            }
+        }
+        for (r = 0; r < p; r++) { free(snap[r]); snap[r] = NULL; }
+    }
+    for (r = 0; r < p; r++) free(partial[r]);
+    free(partial); free(snap);
+    return 0;
+}

@@ -12,6 +12,7 @@
  *   orc_reduce()          intra_Reduce,    src/coll/intra_fns_new.c:4519-4989
  *   orc_reduce_scatter()  intra_Reduce_scatter (commutative branches),
  *                         src/coll/intra_fns_new.c:6191-6503
+ *   orc_scan()            MPIR_intra_Scan, src/coll/intra_scan.c:91-150
  * The collectives are simulated with p in-memory ranks stepping in lockstep
  * through the reference's own send/recv schedule (every round snapshots the
  * senders before any receiver combines), so the combine order, the operand
@@ -50,6 +51,10 @@ int orc_reduce(int p, const void *const *send, void *const *recv,
                int count, int dtype, int op, int root, int *rc);
 int orc_reduce_scatter(int p, const void *const *send, void *const *recv,
                        const int *recvcnts, int dtype, int op, int *rc);
+
+/* MPI_Scan, the default MPIR_intra_Scan (intra_scan.c:91-150) */
+int orc_scan(int p, const void *const *send, void *const *recv, int count,
+             int dtype, int op, int *rc);
 
 /* Which algorithm the reference picks (same thresholds, intra_fns_new.c:
  * 30-40, 123-132, 4619, 5589, 6248, 6450).  Values: see ORC_ALG_*. */

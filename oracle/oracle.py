@@ -41,6 +41,8 @@ def lib():
         L.orc_reduce_scatter.argtypes = [ctypes.c_int, ctypes.POINTER(vp), ctypes.POINTER(vp),
                                          ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.c_int,
                                          ctypes.POINTER(ctypes.c_int)]
+        L.orc_scan.argtypes = [ctypes.c_int, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.c_int,
+                               ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
         L.orc_algorithm.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_long, ctypes.c_int]
         L.orc_fill.argtypes = [vp, ctypes.c_long, ctypes.c_int, ctypes.c_int]
         L.orc_fill.restype = None
@@ -91,6 +93,13 @@ def reduce_scatter(sends, recvs, recvcnts, dtype, op_handle):
     rc = (ctypes.c_int * p)()
     cn = (ctypes.c_int * p)(*recvcnts)
     lib().orc_reduce_scatter(p, _ptrs(sends), _ptrs(recvs), cn, dtype, op_handle, rc)
+    return list(rc)
+
+
+def scan(sends, recvs, count, dtype, op_handle):
+    p = len(sends)
+    rc = (ctypes.c_int * p)()
+    lib().orc_scan(p, _ptrs(sends), _ptrs(recvs), count, dtype, op_handle, rc)
     return list(rc)
 
 

@@ -14,8 +14,9 @@ reduced to data (inputs per rank + the value the reference test asserts):
   answers are size-specific, e.g. LXOR of all-ones is 0 only for even p.)
 * redscat.c (Reduce_scatter SUM INT, recvcounts 1), coll12.c (Reduce MAXLOC /
   Allreduce MINLOC on DOUBLE_INT, TABLE_SIZE 2), redtst.c (BOR: 3|6 == 7),
-  shortint.c (Reduce MINLOC SHORT_INT, root 1): closed forms written out
-  below from the checks those programs make.
+  shortint.c (Reduce MINLOC SHORT_INT, root 1), scantst.c / coll11.c (Scan SUM
+  INT of the rank): closed forms written out below from the checks those
+  programs make.
 
 Only the numbers are committed; no reference source text is.  The temporary
 C program lives in a temp dir and is deleted.
@@ -145,8 +146,14 @@ def main():
                       "inputs": [[[r + i, r] for i in range(10)] for r in range(size)],
                       "expected_root": [[i, 0] for i in range(10)]})
 
+    # scantst.c / coll11.c: data = rank, MPI_Scan SUM INT -> sum_{i<=rank} i
+    for size in range(1, 9):
+        extra.append({"test": "scantst.c", "coll": "scan", "type": "MPI_INT", "op": "MPI_SUM", "size": size,
+                      "count": 1, "inputs": [[r] for r in range(size)],
+                      "expected": [[r * (r + 1) // 2] for r in range(size)]})
+
     doc = {"generated_by": "tests/golden/gen_known_answers.py",
-           "source": "reference examples/test/coll/{allred,redscat,coll12,redtst,shortint}.c",
+           "source": "reference examples/test/coll/{allred,redscat,coll12,redtst,shortint,scantst}.c",
            "allred": {"count": COUNT, "sizes": list(SIZES), "cases": cases},
            "other": extra}
     with open(OUT, "w") as f:

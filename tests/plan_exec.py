@@ -14,8 +14,22 @@ from oracle import oracle as O
 SHAPE_TREE, SHAPE_CHAIN = 0, 1
 
 
-def combine_cpu(op, dtype, esize, leaves, folds, shape, n):
-    """leaves/folds: lists of uint8 arrays (n*esize bytes) or None."""
+def tree_mask(k):
+    m, l = 0, 0
+    while (1 << l) < k and l < 3:
+        for q in range(0, k, 2 << l):
+            if q + (1 << l) < k:
+                m |= 1 << (l * 8 + q)
+        l += 1
+    return m
+
+
+def chain_mask(k):
+    return ((1 << k) - 1) & ~1 if k >= 2 else 0
+
+
+def run_program(op, dtype, leaves, folds, tmask, cmask, n):
+    """The combine program of include/mvx_hip.h, step by step with the oracle op."""
     y = []
     for q, a in enumerate(leaves):
         v = a.copy()
@@ -23,17 +37,22 @@ def combine_cpu(op, dtype, esize, leaves, folds, shape, n):
             O.op(op, dtype, folds[q], v, n)
         y.append(v)
     k = len(y)
-    if shape == SHAPE_CHAIN:
-        for q in range(1, k):
+    for l in range(3):
+        for q in range(8):
+            if tmask >> (l * 8 + q) & 1:
+                assert q + (1 << l) < k
+                O.op(op, dtype, y[q + (1 << l)], y[q], n)
+    for q in range(1, k):
+        if cmask >> q & 1:
             O.op(op, dtype, y[q], y[0], n)
-    else:
-        h = 1
-        while h < k:
-            for q in range(0, k, 2 * h):
-                if q + h < k:
-                    O.op(op, dtype, y[q + h], y[q], n)
-            h *= 2
     return y[0]
+
+
+def combine_cpu(op, dtype, esize, leaves, folds, shape, n):
+    """leaves/folds: lists of uint8 arrays (n*esize bytes) or None."""
+    k = len(leaves)
+    return run_program(op, dtype, leaves, folds, tree_mask(k) if shape == SHAPE_TREE else 0,
+                       chain_mask(k) if shape == SHAPE_CHAIN else 0, n)
 
 
 def run_plans(plans, sends, recvs):
@@ -53,7 +72,7 @@ def run_plans(plans, sends, recvs):
                     assert plans[s].a_send[r].cnt == P.a_recv[s].cnt and plans[s].a_send[r].off == P.a_recv[s].off
         leaves = [sends[P.leaf[q]][lo:hi] for q in range(P.k)]
         folds = [sends[P.leaf_fold[q]][lo:hi] if P.leaf_fold[q] >= 0 else None for q in range(P.k)]
-        out = combine_cpu(P.op, P.dtype, E, leaves, folds, P.shape, P.c_cnt)
+        out = run_program(P.op, P.dtype, leaves, folds, P.tree_mask, P.chain_mask, P.c_cnt)
         outs[r] = out
         if not P.c_dst_tmp:
             d = P.c_dst_off * E

@@ -31,7 +31,7 @@ CASES = [  # (coll, count, dtype, op, root)
     (1, 40000, 17, 111, 0), (1, 20000, 8, 105, 0), (1, 9, 18, 110, 0),
     (2, 10, 6, 102, 0), (2, 30000, 10, 102, 1), (2, 30000, 11, 101, 0), (2, 5000, 17, 110, 1),
     (3, 7, 6, 102, 0), (3, 200, 10, 102, 0), (3, 60000, 10, 102, 0), (3, 60000, 8, 105, 0),
-    (3, 5000, 17, 111, 0),
+    (3, 5000, 17, 111, 0), (4, 10, 6, 102, 0), (4, 3000, 10, 102, 0), (4, 700, 17, 110, 0),
 ]
 
 
@@ -44,7 +44,7 @@ def _worker(rank, world, port, out_dir):
 
     import mvxtest as T
     from oracle import oracle as O
-    from plan_exec import combine_cpu
+    from plan_exec import run_program
 
     mvx = importlib.import_module("mvapich-cce_amd")
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -65,6 +65,11 @@ def _worker(rank, world, port, out_dir):
             R0 = [np.zeros_like(S[0]) for _ in range(world)]
             O.reduce(sb, [x.view(np.uint8) for x in R0], n, dtype, op, root)
             mine = R0[rank] if rank == root else None
+            recvbuf = np.zeros(tot * E, np.uint8)
+        elif coll == 4:
+            R0 = [np.zeros_like(S[0]) for _ in range(world)]
+            O.scan(sb, [x.view(np.uint8) for x in R0], n, dtype, op)
+            mine = R0[rank]
             recvbuf = np.zeros(tot * E, np.uint8)
         else:
             R0 = [np.zeros(max(c, 1), S[0].dtype) for c in cnts]
@@ -93,7 +98,7 @@ def _worker(rank, world, port, out_dir):
                 return send[lo:hi] if s == rank else slot[s].numpy()
             leaves = [leaf(P.leaf[q]) for q in range(P.k)]
             folds = [leaf(P.leaf_fold[q]) if P.leaf_fold[q] >= 0 else None for q in range(P.k)]
-            out = combine_cpu(op, dtype, E, leaves, folds, P.shape, P.c_cnt)
+            out = run_program(op, dtype, leaves, folds, P.tree_mask, P.chain_mask, P.c_cnt)
             if not P.c_dst_tmp:
                 recvbuf[P.c_dst_off * E: P.c_dst_off * E + out.size] = out
         # phase C

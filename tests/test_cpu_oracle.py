@@ -42,6 +42,11 @@ def test_other_reference_tests(oracle):
                                        c["recvcnts"], t, o)
             for r in range(size):
                 assert G.equal(recvs[r], G.to_array(c["expected"][r], c["type"])), c["test"]
+        elif c["coll"] == "scan":
+            recvs = [np.zeros_like(ins[0]) for _ in range(size)]
+            rc = oracle.scan([x.view(np.uint8) for x in ins], [r.view(np.uint8) for r in recvs], c["count"], t, o)
+            for r in range(size):
+                assert G.equal(recvs[r], G.to_array(c["expected"][r], c["type"])), c["test"]
         elif c["coll"] == "allreduce":
             recvs = [np.zeros_like(ins[0]) for _ in range(size)]
             rc = oracle.allreduce([x.view(np.uint8) for x in ins], [r.view(np.uint8) for r in recvs], c["count"], t, o)

@@ -78,6 +78,30 @@ def test_reduce_scatter_plans(mvx, oracle, p, op, dtype):
                 _cmp(op, dtype, R1[r][: cnts[r] * E], R0[r][: cnts[r]])
 
 
+@pytest.mark.parametrize("p", range(1, 9))
+@pytest.mark.parametrize("op,dtype", CASES)
+def test_scan_plans(mvx, oracle, p, op, dtype):
+    """MPI_Scan: rank r's chain of balanced trees (intra_scan.c:118-147)."""
+    for n in (1, 9, 3000):
+        S = [special_vec(dtype, n, 3 * p + 11 * r + n) for r in range(p)]
+        R0 = [np.zeros_like(S[0]) for _ in range(p)]
+        rc = oracle.scan([s.view(np.uint8) for s in S], [x.view(np.uint8) for x in R0], n, dtype, op)
+        plans = [mvx.plan(mvx.COLL_SCAN, p, r, n, dtype, op) for r in range(p)]
+        assert [P.k for P in plans] == [r + 1 for r in range(p)]
+        R1 = run_plans(plans, [s.view(np.uint8) for s in S], [np.zeros(S[0].nbytes, np.uint8) for _ in range(p)])
+        for r in range(p):
+            _cmp(op, dtype, R1[r], R0[r])
+        assert rc == [0] * p
+
+
+def test_scan_undefined_op_is_not_an_error(oracle):
+    """MPIR_intra_Scan never reports MPIR_Op_errno (intra_scan.c:143-150)."""
+    x = [np.arange(4, dtype=np.float32).view(np.uint8) for _ in range(4)]
+    y = [np.zeros(4, np.float32).view(np.uint8) for _ in range(4)]
+    assert oracle.scan(x, y, 4, 10, 105) == [0] * 4
+    assert all(np.array_equal(a, b) for a, b in zip(x, y))
+
+
 def test_algorithm_thresholds(mvx, oracle):
     """coll_table (intra_fns_new.c:129-132) and the Reduce_scatter 512 KiB
     switch (:39, :6248): plan and oracle agree at and around every edge."""

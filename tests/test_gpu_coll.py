@@ -73,6 +73,23 @@ def test_reduce_matches_reference_schedule(mvx, oracle, comms, p, op, dtype):
 
 @pytest.mark.parametrize("p", [1, 2, 3, 4, 5, 6, 7, 8])
 @pytest.mark.parametrize("op,dtype", CASES)
+def test_scan_matches_reference_schedule(mvx, oracle, comms, p, op, dtype):
+    import torch
+    for n in (1, 10, 5000, 70001):
+        sends = [T.rand_vec(dtype, n, 7 * p + 3 * r + n) for r in range(p)]
+        ds = [T.to_dev(s) for s in sends]
+        drs = [torch.zeros(sends[0].nbytes, dtype=torch.uint8, device="cuda") for _ in range(p)]
+        r, rcs = comms[p].scan_multi(ds, drs, n, dtype, op)
+        assert r == 0
+        refs = [np.zeros_like(sends[0]) for _ in range(p)]
+        rref = oracle.scan([s.view(np.uint8) for s in sends], [x.view(np.uint8) for x in refs], n, dtype, op)
+        assert rcs == rref
+        for q in range(p):
+            T.assert_same(op, dtype, T.from_dev(drs[q]), refs[q], typemap_only=True)
+
+
+@pytest.mark.parametrize("p", [1, 2, 3, 4, 5, 6, 7, 8])
+@pytest.mark.parametrize("op,dtype", CASES)
 def test_reduce_scatter_matches_reference_schedule(mvx, oracle, comms, p, op, dtype):
     for base in (0, 1, 3, 500, 20000, 70000):
         cnts = [max(0, base + (r % 3) - 1) for r in range(p)]
@@ -168,6 +185,13 @@ def test_rccl_single_rank_world(mvx, oracle):
     hs = np.zeros(n, np.float32)
     assert mvx.MPI_Reduce_scatter(a, hs, [n], 10, 102, comm) == 0
     assert np.array_equal(hs, a)
+    hc = np.zeros(n, np.float32)
+    assert mvx.MPI_Scan(a, hc, n, 10, 102, comm) == 0
+    assert np.array_equal(hc, a)
+    dc = torch.zeros_like(da)
+    assert comm.scan_async(da, dc, n, 10, 102) == 0
+    torch.cuda.synchronize()
+    assert np.array_equal(dc.cpu().numpy(), a)
     # argument errors: reference order and codes
     code = mvx.MPI_Allreduce(da, da, n, 10, 102, comm)
     assert mvx.error_class(code) == mvx.MPI_ERR_BUFFER and (code >> 6) & 0x7f == 7

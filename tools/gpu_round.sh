@@ -37,3 +37,10 @@ if [[ $STAGE == all || $STAGE == host ]]; then
   run timeout -k 10 300 python tools/bench_host.py > gpurun_out/bench_host.jsonl 2> gpurun_out/bench_host.err || { tail -20 gpurun_out/bench_host.err; exit 1; }
   cat gpurun_out/bench_host.jsonl
 fi
+if [[ $STAGE == kernels_ab ]]; then
+  run timeout -k 10 300 python tools/bench_kernels.py > gpurun_out/bench_kernels_u2.jsonl 2> gpurun_out/bench_kernels.err || exit 1
+  MVX_PROG_U1=1 run timeout -k 10 300 python tools/bench_kernels.py > gpurun_out/bench_kernels_u1.jsonl 2>> gpurun_out/bench_kernels.err || exit 1
+  run timeout -k 10 300 python tools/bench_kernels.py > gpurun_out/bench_kernels_u2b.jsonl 2>> gpurun_out/bench_kernels.err || exit 1
+  MVX_PROG_U1=1 run timeout -k 10 300 python tools/bench_kernels.py > gpurun_out/bench_kernels_u1b.jsonl 2>> gpurun_out/bench_kernels.err || exit 1
+  for f in u2 u1 u2b u1b; do echo "-- $f"; cut -c1-200 gpurun_out/bench_kernels_$f.jsonl; done
+fi
