@@ -355,7 +355,6 @@ typedef void (*KFn)(const Params);
 struct KSet {
     const void *apply[2];  // KMAX 2 (k <= 2), 4 chunks in flight per lane; [NT]
     const void *prog[2];   // KMAX 8 combine program
-    const void *prog1[2];  // the same with one chunk in flight (A/B knob)
     int prog_unroll;       // its chunks in flight per lane
     int esize;
     const char *name;
@@ -367,14 +366,16 @@ static KSet kset(const char *name)
     KSet s;
     s.apply[0] = (const void *)&k_combine<O, T, 2, 4, 0>;
     s.apply[1] = (const void *)&k_combine<O, T, 2, 4, 1>;
-    // 1- and 2-byte elements unpack to 16 or 8 values per chunk: one chunk in
-    // flight keeps those programs in registers (two spill to scratch)
-    constexpr int UP = sizeof(T) >= 4 ? 2 : 1;
+    // chunks in flight per lane, measured (tools/bench_kernels.py, A/B in one
+    // box): 4-byte elements 2 (config-3 tree 52.4 vs 53.0 us), 8-byte
+    // elements 1 (config-4 chain 217 vs 234 us, config-5 MAXLOC 102 vs
+    // 113 us); 1- and 2-byte elements unpack to 16 or 8 values per chunk and
+    // spill to scratch at 2
+    constexpr int UP = sizeof(T) == 4 ? 2 : 1;
     s.prog[0] = (const void *)&k_combine<O, T, MVX_COMBINE_KMAX, UP, 0>;
     s.prog[1] = (const void *)&k_combine<O, T, MVX_COMBINE_KMAX, UP, 1>;
     s.prog_unroll = UP;
-    s.prog1[0] = (const void *)&k_combine<O, T, MVX_COMBINE_KMAX, 1, 0>;
-    s.prog1[1] = (const void *)&k_combine<O, T, MVX_COMBINE_KMAX, 1, 1>;
+
     s.esize = (int)sizeof(T);
     s.name = name;
     return s;
@@ -505,7 +506,6 @@ static int g_block_cap = 1 << 20;
 static long g_nt_min_bytes = 64L << 20;
 static const char *g_last = "";
 static char g_last_buf[96];
-static int g_prog_u1 = 0;   // MVX_PROG_U1=1: program kernels with one chunk in flight
 
 static void init_env()
 {
@@ -514,8 +514,6 @@ static void init_env()
     done = 1;
     const char *e = getenv("MVX_NT_MIN_BYTES");
     if (e) g_nt_min_bytes = atol(e);
-    e = getenv("MVX_PROG_U1");
-    if (e) g_prog_u1 = atoi(e);
     e = getenv("MVX_BLOCK_CAP");
     if (e && atoi(e) > 0) g_block_cap = atoi(e);
 }
@@ -621,7 +619,6 @@ extern "C" int mvx_op_program(int op, int dtype, const void *const *srcs,
         if (k == 2 && !(tree_mask & 1u) && !(chain_mask & 2u)) return MPI_ERR_ARG;
         return launch(ks, ks->apply, 4, P, (hipStream_t)stream);
     }
-    if (g_prog_u1) return launch(ks, ks->prog1, 1, P, (hipStream_t)stream);
     return launch(ks, ks->prog, ks->prog_unroll, P, (hipStream_t)stream);
 }
 

@@ -262,14 +262,12 @@ void orc_fill(void *buf, long n, int dist, int rank)
         for (i = 0; i < n; i++)
             f[i] = (float)((xs64(&s) >> 40) * (1.0 / 16777216.0));
         break; }
-    case 2: { /* int64 words with P(bit = 1) = 0.95 */
+    case 2: { /* int64 words, P(bit = 1) = 1 - (1/16)(1/4) = 0.953 (six draws) */
         uint64_t *w = (uint64_t *)buf;
         for (i = 0; i < n; i++) {
-            uint64_t v = ~0ULL;
-            int bit;
-            for (bit = 0; bit < 64; bit++)
-                if (xs64(&s) % 100ULL < 5ULL) v &= ~(1ULL << bit);
-            w[i] = v;
+            uint64_t a = xs64(&s), b = xs64(&s), c = xs64(&s), d = xs64(&s);
+            uint64_t e = xs64(&s), f = xs64(&s);
+            w[i] = a | b | c | d | (e & f);
         }
         break; }
     case 3: case 4: { /* FLOAT_INT pairs with many ties */

@@ -71,7 +71,7 @@ int orc_algorithm(int coll, int p, long total_count, int dtype);
 
 /* Synthetic input generator: xorshift64 seeded
  * 0x9E3779B97F4A7C15 ^ (rank*1000003 + 1).  dist: 0 mixed-sign f32,
- * 1 U[0,1) f32, 2 int64 with P(bit)=0.95, 3 FLOAT_INT v=u%1024 l=rank,
+ * 1 U[0,1) f32, 2 int64 with P(bit)=0.953, 3 FLOAT_INT v=u%1024 l=rank,
  * 4 FLOAT_INT v=u%1024 l=rank*n+i, 5 raw 64-bit words (any type). */
 void orc_fill(void *buf, long n, int dist, int rank);
 

@@ -208,3 +208,53 @@ def test_rccl_single_rank_world(mvx, oracle):
     torch.cuda.synchronize()
     assert np.array_equal(db.cpu().numpy(), a)
     comm.free()
+
+
+def _full_size(mvx, oracle, comms, coll, p, n_elems, dtype, op, dist, cnts=None):
+    """Every rank of a BASELINE config at its full size, on one GPU's HBM."""
+    import torch
+    npdt = T.np_dtype(dtype)
+    sends = []
+    for r in range(p):
+        a = np.empty(n_elems, npdt)
+        oracle.fill(a, n_elems, dist, r)
+        sends.append(a)
+    ds = [torch.from_numpy(a.view(np.uint8)).cuda() for a in sends]
+    if coll == "rs":
+        drs = [torch.empty(c * npdt.itemsize, dtype=torch.uint8, device="cuda") for c in cnts]
+        r, rcs = comms[p].reduce_scatter_multi(ds, drs, cnts, dtype, op)
+        refs = [np.zeros(c, npdt) for c in cnts]
+        rref = oracle.reduce_scatter([s.view(np.uint8) for s in sends], [x.view(np.uint8) for x in refs], cnts,
+                                     dtype, op)
+    else:
+        drs = [torch.empty(n_elems * npdt.itemsize, dtype=torch.uint8, device="cuda") for _ in range(p)]
+        r, rcs = comms[p].allreduce_multi(ds, drs, n_elems, dtype, op)
+        refs = [np.zeros(n_elems, npdt) for _ in range(p)]
+        rref = oracle.allreduce([s.view(np.uint8) for s in sends], [x.view(np.uint8) for x in refs], n_elems,
+                                dtype, op)
+    assert r == 0 and rcs == rref == [0] * p
+    del ds
+    for q in range(p):
+        got = T.from_dev(drs[q])
+        T.assert_same(op, dtype, got, refs[q], typemap_only=True)
+        drs[q] = None
+    torch.cuda.empty_cache()
+
+
+def test_c3_full_size_allreduce_sum_f32_8x256mib(mvx, oracle, comms):
+    """Config 3 at full size: 8 ranks x 256 MiB MPI_FLOAT MPI_SUM,
+    Rabenseifner order, bit-exact on every rank."""
+    _full_size(mvx, oracle, comms, "ar", 8, 64 << 20, 10, 102, 0)
+
+
+def test_c4_full_size_reduce_scatter_band_int64_4x1gib(mvx, oracle, comms):
+    """Config 4 at full size: 4 ranks x 1 GiB MPI_LONG MPI_BAND (pairwise
+    chain), recvcnts 33554432 x 4, bit-exact."""
+    n = 1 << 27
+    _full_size(mvx, oracle, comms, "rs", 4, n, 8, 105, 2, cnts=[n // 4] * 4)
+
+
+def test_c5_full_size_allreduce_maxloc_float_int_8x64mi(mvx, oracle, comms):
+    """Config 5 at full size: 8 ranks x 64 Mi MPI_FLOAT_INT pairs MPI_MAXLOC
+    with many ties (v = u % 1024, loc = rank*n + i), bit-exact."""
+    _full_size(mvx, oracle, comms, "ar", 8, 64 << 20, 17, 111, 4)
