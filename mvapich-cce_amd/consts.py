@@ -32,6 +32,9 @@ PAIR_DOUBLE_INT = np.dtype({"names": ["v", "l"], "formats": [np.float64, np.int3
 PAIR_LONG_INT = np.dtype({"names": ["v", "l"], "formats": [np.int64, np.int32], "offsets": [0, 8], "itemsize": 16})
 PAIR_SHORT_INT = np.dtype({"names": ["v", "l"], "formats": [np.int16, np.int32], "offsets": [0, 4], "itemsize": 8})
 PAIR_2INT = np.dtype([("v", np.int32), ("l", np.int32)])
+# x87 80-bit long double in a 16-byte slot (x86-64 numpy longdouble)
+PAIR_LONG_DOUBLE_INT = np.dtype({"names": ["v", "l"], "formats": [np.longdouble, np.int32], "offsets": [0, 16],
+                                 "itemsize": 32})
 
 NP_DTYPE = {
     MPI_CHAR: np.dtype(np.int8), MPI_UNSIGNED_CHAR: np.dtype(np.uint8), MPI_BYTE: np.dtype(np.uint8),
@@ -42,6 +45,7 @@ NP_DTYPE = {
     MPI_COMPLEX: np.dtype(np.complex64), MPI_DOUBLE_COMPLEX: np.dtype(np.complex128),
     MPI_FLOAT_INT: PAIR_FLOAT_INT, MPI_DOUBLE_INT: PAIR_DOUBLE_INT, MPI_LONG_INT: PAIR_LONG_INT,
     MPI_SHORT_INT: PAIR_SHORT_INT, MPI_2INT: PAIR_2INT,
+    MPI_LONG_DOUBLE: np.dtype(np.longdouble), MPI_LONG_DOUBLE_INT: PAIR_LONG_DOUBLE_INT,
 }
 
 OP_NAMES = {MPI_MAX: "MPI_MAX", MPI_MIN: "MPI_MIN", MPI_SUM: "MPI_SUM", MPI_PROD: "MPI_PROD",
@@ -59,8 +63,8 @@ TYPE_NAMES = {MPI_CHAR: "MPI_CHAR", MPI_UNSIGNED_CHAR: "MPI_UNSIGNED_CHAR", MPI_
 # (op, type) pairs the reference defines (global_ops.c)
 _INTS = [MPI_CHAR, MPI_UNSIGNED_CHAR, MPI_SHORT, MPI_UNSIGNED_SHORT, MPI_INT, MPI_UNSIGNED, MPI_LONG,
          MPI_UNSIGNED_LONG, MPI_LONG_LONG_INT]
-_FLTS = [MPI_FLOAT, MPI_DOUBLE]
-_PAIRS = [MPI_FLOAT_INT, MPI_DOUBLE_INT, MPI_LONG_INT, MPI_SHORT_INT, MPI_2INT]
+_FLTS = [MPI_FLOAT, MPI_DOUBLE, MPI_LONG_DOUBLE]
+_PAIRS = [MPI_FLOAT_INT, MPI_DOUBLE_INT, MPI_LONG_INT, MPI_SHORT_INT, MPI_2INT, MPI_LONG_DOUBLE_INT]
 DEFINED = {
     MPI_MAX: _INTS + _FLTS, MPI_MIN: _INTS + _FLTS,
     MPI_SUM: _INTS + _FLTS + [MPI_COMPLEX, MPI_DOUBLE_COMPLEX],

@@ -33,6 +33,7 @@
 
 #include "mvx_mpi.h"
 #include "mvx_hip.h"
+#include "mvx_xf80.h"
 
 namespace mvx {
 
@@ -53,12 +54,11 @@ struct psi { int16_t v; int16_t pad; int32_t l; };      // 8 B
 struct pii { int32_t v; int32_t l; };                   // MPI_2INT
 static_assert(sizeof(pdi) == 16 && sizeof(pli) == 16 && sizeof(psi) == 8, "");
 
-template <typename T> struct is_pair { static constexpr bool value = false; };
-template <> struct is_pair<pfi> { static constexpr bool value = true; };
-template <> struct is_pair<pdi> { static constexpr bool value = true; };
-template <> struct is_pair<pli> { static constexpr bool value = true; };
-template <> struct is_pair<psi> { static constexpr bool value = true; };
-template <> struct is_pair<pii> { static constexpr bool value = true; };
+// x87 long double (16-byte slot) and MPI_LONG_DOUBLE_INT (32 bytes):
+// integer emulation of the x87 unit, mvx_xf80.h
+using xf::xf80;
+using xf::pxi;
+static_assert(sizeof(xf80) == 16 && sizeof(pxi) == 32, "");
 
 // ---------------------------------------------------------------------------
 // the ops: F<op, T>::f(a, b) returns the new inout value (a = inout, b = in)
@@ -142,6 +142,18 @@ template <typename T> struct F<OMINLOC, T> {
     static __device__ __forceinline__ T f(T a, T b) { return loc_op<T, true>(a, b); }
 };
 
+// the x87 types (global_ops.c:149-155 and the HAVE_LONG_DOUBLE case of every
+// op; 1365-1378 / 1605-1618 for LONG_DOUBLE_INT)
+template <> struct F<OMAX, xf80> { static __device__ __forceinline__ xf80 f(xf80 a, xf80 b) { return xf::max(a, b); } };
+template <> struct F<OMIN, xf80> { static __device__ __forceinline__ xf80 f(xf80 a, xf80 b) { return xf::min(a, b); } };
+template <> struct F<OSUM, xf80> { static __device__ __forceinline__ xf80 f(xf80 a, xf80 b) { return xf::add(a, b); } };
+template <> struct F<OPROD, xf80> { static __device__ __forceinline__ xf80 f(xf80 a, xf80 b) { return xf::mul(a, b); } };
+template <> struct F<OLAND, xf80> { static __device__ __forceinline__ xf80 f(xf80 a, xf80 b) { return xf::land(a, b); } };
+template <> struct F<OLOR, xf80> { static __device__ __forceinline__ xf80 f(xf80 a, xf80 b) { return xf::lor(a, b); } };
+template <> struct F<OLXOR, xf80> { static __device__ __forceinline__ xf80 f(xf80 a, xf80 b) { return xf::lxor(a, b); } };
+template <> struct F<OMAXLOC, pxi> { static __device__ __forceinline__ pxi f(pxi a, pxi b) { return xf::loc<false>(a, b); } };
+template <> struct F<OMINLOC, pxi> { static __device__ __forceinline__ pxi f(pxi a, pxi b) { return xf::loc<true>(a, b); } };
+
 // ---------------------------------------------------------------------------
 // launch parameters (passed by value, ~170 bytes of kernarg)
 
@@ -151,7 +163,7 @@ struct Params {
     char *dst;
     long n;      // elements
     long head;   // scalar elements before the 16-byte aligned body
-    long nvec;   // 16-byte chunks in the body
+    long nvec;   // chunks in the body (16 bytes, or one element if wider)
     int k;       // leaves
     int vec_ok;  // all pointers share their alignment mod 16
     unsigned tree_mask;   // bit l*8+q: y[q] = op(y[q], y[q + 2^l]), levels 0..2
@@ -160,28 +172,20 @@ struct Params {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));  // one dwordx4
 
-// 16 bytes of elements; moved to/from the dwordx4 registers by memcpy (a
-// well-defined bit copy that keeps pair padding bytes; union punning lets
-// clang drop the element writes).
-template <typename T> struct Chunk {
-    T e[16 / sizeof(T)];
+// A chunk is what one lane moves per operand per step: 16 bytes of
+// elements, or one element of a wider type (MPI_LONG_DOUBLE_INT, 32 bytes:
+// two dwordx4).  Moved to/from the registers by memcpy (a well-defined bit
+// copy that keeps pair padding bytes; union punning lets clang drop the
+// element writes).
+template <typename T> struct CG {
+    static constexpr int bytes = sizeof(T) > 16 ? (int)sizeof(T) : 16;
+    static constexpr int w = bytes / 16;          // dwordx4 per chunk
+    static constexpr int v = bytes / (int)sizeof(T);  // elements per chunk
 };
 
-template <typename T>
-__device__ __forceinline__ Chunk<T> unpack(u32x4 r)
-{
-    Chunk<T> c;
-    __builtin_memcpy(&c, &r, 16);
-    return c;
-}
-
-template <typename T>
-__device__ __forceinline__ u32x4 pack(const Chunk<T> &c)
-{
-    u32x4 r;
-    __builtin_memcpy(&r, &c, 16);
-    return r;
-}
+template <typename T> struct Chunk {
+    T e[CG<T>::v];
+};
 
 // whole-element store: the pair padding is an explicit member carried from
 // leaf 0, so the element path writes the same bytes as the 16-byte path
@@ -244,11 +248,31 @@ __device__ __forceinline__ void st(u32x4 *p, u32x4 v)
     else *p = v;
 }
 
+template <typename T, int NT>
+__device__ __forceinline__ Chunk<T> ld_chunk(const u32x4 *base, long c)
+{
+    u32x4 r[CG<T>::w];
+#pragma unroll
+    for (int w = 0; w < CG<T>::w; ++w) r[w] = ld<NT>(base + c * CG<T>::w + w);
+    Chunk<T> x;
+    __builtin_memcpy(&x, r, sizeof x);
+    return x;
+}
+
+template <typename T, int NT>
+__device__ __forceinline__ void st_chunk(u32x4 *base, long c, const Chunk<T> &x)
+{
+    u32x4 r[CG<T>::w];
+    __builtin_memcpy(r, &x, sizeof x);
+#pragma unroll
+    for (int w = 0; w < CG<T>::w; ++w) st<NT>(base + c * CG<T>::w + w, r[w]);
+}
+
 template <int O, typename T, int KMAX, int U, int NT>
 __global__ void __launch_bounds__(256)
 k_combine(const Params P)
 {
-    constexpr int V = 16 / sizeof(T);
+    constexpr int V = CG<T>::v;
     const long tid = (long)blockIdx.x * 256 + threadIdx.x;
     const long nthr = (long)gridDim.x * 256;
 
@@ -284,7 +308,7 @@ k_combine(const Params P)
             if (c < P.nvec) {
 #pragma unroll
                 for (int q = 0; q < KMAX; ++q)
-                    if (q < k) x[u][q] = unpack<T>(ld<NT>(src[q] + c));
+                    if (q < k) x[u][q] = ld_chunk<T, NT>(src[q], c);
             }
         }
 #pragma unroll
@@ -294,7 +318,7 @@ k_combine(const Params P)
                 for (int u = 0; u < U; ++u) {
                     const long c = c0 + (long)u * 256;
                     if (c < P.nvec) {
-                        const Chunk<T> f = unpack<T>(ld<NT>(fold[q] + c));
+                        const Chunk<T> f = ld_chunk<T, NT>(fold[q], c);
 #pragma unroll
                         for (int j = 0; j < V; ++j) x[u][q].e[j] = F<O, T>::f(x[u][q].e[j], f.e[j]);
                     }
@@ -338,7 +362,7 @@ k_combine(const Params P)
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const long c = c0 + (long)u * 256;
-            if (c < P.nvec) st<NT>(dst + c, pack<T>(x[u][0]));
+            if (c < P.nvec) st_chunk<T, NT>(dst, c, x[u][0]);
         }
     }
 }
@@ -357,6 +381,7 @@ struct KSet {
     const void *prog[2];   // KMAX 8 combine program
     int prog_unroll;       // its chunks in flight per lane
     int esize;
+    int chunk;             // bytes per chunk (16, or the element if wider)
     const char *name;
 };
 
@@ -377,6 +402,7 @@ static KSet kset(const char *name)
     s.prog_unroll = UP;
 
     s.esize = (int)sizeof(T);
+    s.chunk = CG<T>::bytes;
     s.name = name;
     return s;
 }
@@ -449,11 +475,15 @@ static int ek_size(int ek)
     case EK_PSI: { static KSet s = kset<O, psi>(NAME "_short_int"); return &s; } \
     case EK_PII: { static KSet s = kset<O, pii>(NAME "_2int"); return &s; }
 
+#define LDBL(O, NAME)                                                        \
+    case EK_LDBL: { static KSet s = kset<O, xf80>(NAME "_f80"); return &s; }
+#define LDBL_INT(O, NAME)                                                    \
+    case EK_LDBL_INT: { static KSet s = kset<O, pxi>(NAME "_long_double_int"); return &s; }
+
 // Returns the kernel set, or NULL with *rc set to the reference's answer for
 // that (op, type): 329 where the op's switch has no case for it
-// (global_ops.c:158-161 and every sibling default), MPI_ERR_TYPE where it has
-// one but the type has no device representation (x87 long double), and
-// MPI_ERR_OP for a handle outside MPI_MAX..MPI_MAXLOC.
+// (global_ops.c:158-161 and every sibling default), and MPI_ERR_OP for a
+// handle outside MPI_MAX..MPI_MAXLOC.
 static const KSet *lookup(int op, int dtype, int *rc)
 {
     const int ek = ekind(dtype);
@@ -461,25 +491,25 @@ static const KSet *lookup(int op, int dtype, int *rc)
     switch (op) {
     case MPI_MAX:
         switch (ek) { SIGNED_INT(OMAX, "max") FLOATS(OMAX, "max")
-        case EK_LDBL: *rc = MPI_ERR_TYPE; return nullptr; default: return nullptr; }
+        LDBL(OMAX, "max") default: return nullptr; }
     case MPI_MIN:
         switch (ek) { SIGNED_INT(OMIN, "min") FLOATS(OMIN, "min")
-        case EK_LDBL: *rc = MPI_ERR_TYPE; return nullptr; default: return nullptr; }
+        LDBL(OMIN, "min") default: return nullptr; }
     case MPI_SUM:
         switch (ek) { ARITH_INT(OSUM, "sum") FLOATS(OSUM, "sum") CMPLX(OSUM, "sum")
-        case EK_LDBL: *rc = MPI_ERR_TYPE; return nullptr; default: return nullptr; }
+        LDBL(OSUM, "sum") default: return nullptr; }
     case MPI_PROD:
         switch (ek) { ARITH_INT(OPROD, "prod") FLOATS(OPROD, "prod") CMPLX(OPROD, "prod")
-        case EK_LDBL: *rc = MPI_ERR_TYPE; return nullptr; default: return nullptr; }
+        LDBL(OPROD, "prod") default: return nullptr; }
     case MPI_LAND:
         switch (ek) { ARITH_INT(OLAND, "land") FLOATS(OLAND, "land")
-        case EK_LDBL: *rc = MPI_ERR_TYPE; return nullptr; default: return nullptr; }
+        LDBL(OLAND, "land") default: return nullptr; }
     case MPI_LOR:
         switch (ek) { ARITH_INT(OLOR, "lor") FLOATS(OLOR, "lor")
-        case EK_LDBL: *rc = MPI_ERR_TYPE; return nullptr; default: return nullptr; }
+        LDBL(OLOR, "lor") default: return nullptr; }
     case MPI_LXOR:
         switch (ek) { ARITH_INT(OLXOR, "lxor") FLOATS(OLXOR, "lxor")
-        case EK_LDBL: *rc = MPI_ERR_TYPE; return nullptr; default: return nullptr; }
+        LDBL(OLXOR, "lxor") default: return nullptr; }
     case MPI_BAND:
         switch (ek) { case EK_BYTE: ARITH_INT(OBAND, "band") default: return nullptr; }
     case MPI_BOR:
@@ -488,10 +518,10 @@ static const KSet *lookup(int op, int dtype, int *rc)
         switch (ek) { case EK_BYTE: ARITH_INT(OBXOR, "bxor") default: return nullptr; }
     case MPI_MAXLOC:
         switch (ek) { PAIRS(OMAXLOC, "maxloc")
-        case EK_LDBL_INT: *rc = MPI_ERR_TYPE; return nullptr; default: return nullptr; }
+        LDBL_INT(OMAXLOC, "maxloc") default: return nullptr; }
     case MPI_MINLOC:
         switch (ek) { PAIRS(OMINLOC, "minloc")
-        case EK_LDBL_INT: *rc = MPI_ERR_TYPE; return nullptr; default: return nullptr; }
+        LDBL_INT(OMINLOC, "minloc") default: return nullptr; }
     default:
         *rc = MPI_ERR_OP;
         return nullptr;
@@ -538,7 +568,7 @@ static int launch(const KSet *ks, const void *const fns[2], int unroll, Params &
         long head = pre / es;
         if (head > P.n) head = P.n;
         P.head = head;
-        P.nvec = (P.n - head) * es / 16;
+        P.nvec = (P.n - head) * es / ks->chunk;
         P.vec_ok = 1;
     } else {
         P.head = 0;

@@ -128,11 +128,14 @@ int mvx_plan_algorithm(int coll, int p, long total, int dtype)
     }
 }
 
-/* Does the op's result depend on which operand is inout?  Only for the
- * IEEE compare-select ops, where NaN and +-0 pick an operand by role
- * (coll.h:14-19, global_ops.c:1297-1309). */
+/* Does the op's result depend on which operand is inout?  For the IEEE
+ * compare-select ops, where NaN and +-0 pick an operand by role (coll.h:14-19,
+ * global_ops.c:1297-1309), and for every op on the x87 types: an x87 store
+ * writes 10 bytes, so the 6 padding bytes of the 16-byte slot, which
+ * MPI_LONG_DOUBLE's type map moves, stay those of the inout operand. */
 static int op_symmetric(int op, int dtype)
 {
+    if (dtype == MPI_LONG_DOUBLE || dtype == MPI_LONG_DOUBLE_INT) return 0;
     switch (op) {
     case MPI_SUM: case MPI_PROD: case MPI_LAND: case MPI_LOR: case MPI_LXOR:
     case MPI_BAND: case MPI_BOR: case MPI_BXOR:

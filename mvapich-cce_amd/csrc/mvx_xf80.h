@@ -1,0 +1,270 @@
+// mvx_xf80.h -- x87 80-bit extended precision (`long double` on x86-64) in
+// integer arithmetic, for MPI_LONG_DOUBLE / MPI_LONG_DOUBLE_INT on the
+// device.
+//
+// The reference evaluates these types with the host's x87 unit
+// (global_ops.c:149-155, 259-265, 376-382, 504-510, 637-643, 866-872,
+// 1095-1101, 1365-1378, 1605-1618), under the x86-64 Linux default control
+// word: 64-bit precision, round to nearest even, every exception masked.  The
+// functions here reproduce that bit for bit, including what the masked
+// exceptions leave behind:
+//   * unsupported encodings (unnormals, pseudo-infinities, pseudo-NaNs) are
+//     invalid operands: arithmetic returns the real indefinite QNaN
+//     (sign 1, exponent 0x7fff, significand 0xC000000000000000) and every
+//     comparison is unordered;
+//   * pseudo-denormals (exponent 0, integer bit 1) are read as the
+//     denormal exponent;
+//   * inf - inf and 0 * inf give the real indefinite;
+//   * a NaN operand propagates quieted.  Between two NaNs a QNaN beats an
+//     SNaN, and between NaNs of one kind the larger significand wins (Intel
+//     SDM vol. 1 table 4-7, x87 column);
+//   * a tiny result is denormalised with one rounding at the denormal
+//     position (masked underflow), and overflow gives infinity.
+// tests/test_cpu_xf80.py checks all of this against this container's x87.
+//
+// Both host and device code compile this header: the host build is the
+// fuzz harness that checks it against the oracle's x87.
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#define XF_FN __host__ __device__ __forceinline__
+#else
+#define XF_FN static inline
+#endif
+
+namespace xf {
+
+// one MPI_LONG_DOUBLE element: the 10 bytes x87 stores plus the 6 bytes of
+// its 16-byte slot, which an x87 store never writes (carried from the inout
+// operand)
+struct xf80 {
+    uint64_t m;      // significand, explicit integer bit 63
+    uint16_t se;     // sign 15, biased exponent 14..0
+    uint16_t pad0;
+    uint32_t pad1;
+};
+
+typedef unsigned __int128 u128;
+
+enum { K_ZERO = 0, K_FIN, K_INF, K_QNAN, K_SNAN, K_BAD };
+
+XF_FN int klass(uint64_t m, uint32_t e)
+{
+    const bool j = (m >> 63) != 0;
+    if (e == 0x7fff) {
+        if (!j) return K_BAD;                       // pseudo-infinity / pseudo-NaN
+        if ((m << 1) == 0) return K_INF;
+        return (m >> 62) & 1 ? K_QNAN : K_SNAN;
+    }
+    if (e == 0) return m == 0 ? K_ZERO : K_FIN;     // denormal or pseudo-denormal
+    return j ? K_FIN : K_BAD;                       // unnormal
+}
+
+XF_FN xf80 with_bits(xf80 pads, uint64_t m, uint32_t se)
+{
+    xf80 r = pads;
+    r.m = m;
+    r.se = (uint16_t)se;
+    return r;
+}
+
+XF_FN xf80 indefinite(xf80 pads) { return with_bits(pads, 0xC000000000000000ull, 0xffff); }
+
+// result of an arithmetic op with a NaN operand (and no invalid encoding)
+XF_FN xf80 nan_result(xf80 a, int ka, xf80 b, int kb)
+{
+    const bool na = ka == K_QNAN || ka == K_SNAN, nb = kb == K_QNAN || kb == K_SNAN;
+    uint64_t m;
+    uint32_t se;
+    if (na && nb) {
+        if (ka != kb) {                              // the QNaN wins
+            m = ka == K_QNAN ? a.m : b.m;
+            se = ka == K_QNAN ? a.se : b.se;
+        } else if (a.m != b.m) {                     // larger significand
+            m = a.m > b.m ? a.m : b.m;
+            se = a.m > b.m ? a.se : b.se;
+        } else {                                     // equal: ties go to b... see tests
+            m = a.m;
+            se = (a.se & b.se & 0x8000) | 0x7fff;
+        }
+    } else if (na) {
+        m = a.m;
+        se = a.se;
+    } else {
+        m = b.m;
+        se = b.se;
+    }
+    return with_bits(a, m | (1ull << 62), se);
+}
+
+XF_FN int clz128(u128 x)
+{
+    const uint64_t hi = (uint64_t)(x >> 64), lo = (uint64_t)x;
+    return hi ? __builtin_clzll(hi) : (lo ? 64 + __builtin_clzll(lo) : 128);
+}
+
+// round S (binary point after bit 64: significand = S >> 64) to 64 bits,
+// nearest even, at effective exponent e >= 1; encode with sign s
+XF_FN xf80 round_pack(xf80 pads, uint32_t s, int e, u128 S)
+{
+    uint64_t r = (uint64_t)(S >> 64);
+    const uint64_t low = (uint64_t)S;
+    if ((low >> 63) && ((low << 1) || (r & 1))) {
+        if (++r == 0) {
+            r = 1ull << 63;
+            ++e;
+        }
+    }
+    if (e >= 0x7fff) return with_bits(pads, 1ull << 63, (s << 15) | 0x7fff);   // overflow
+    const uint32_t enc = (r >> 63) ? (uint32_t)e : 0u;                          // denormal
+    return with_bits(pads, r, (s << 15) | enc);
+}
+
+// a + b (the reference's `a[i] = a[i] + b[i]`); pads from a
+XF_FN xf80 add(xf80 a, xf80 b)
+{
+    const uint32_t ea = a.se & 0x7fff, eb = b.se & 0x7fff;
+    uint32_t sa = a.se >> 15, sb = b.se >> 15;
+    const int ka = klass(a.m, ea), kb = klass(b.m, eb);
+    if (ka == K_BAD || kb == K_BAD) return indefinite(a);
+    if (ka >= K_QNAN || kb >= K_QNAN) return nan_result(a, ka, b, kb);
+    if (ka == K_INF || kb == K_INF) {
+        if (ka == K_INF && kb == K_INF && sa != sb) return indefinite(a);
+        return ka == K_INF ? with_bits(a, a.m, a.se) : with_bits(a, b.m, b.se);
+    }
+    if (ka == K_ZERO && kb == K_ZERO) return with_bits(a, 0, (sa & sb) << 15);
+    int xa = ea ? (int)ea : 1, xb = eb ? (int)eb : 1;
+    uint64_t ma = a.m, mb = b.m;
+    if (xb > xa || (xb == xa && mb > ma)) {          // |a| >= |b| from here
+        const int t = xa; xa = xb; xb = t;
+        const uint64_t tm = ma; ma = mb; mb = tm;
+        const uint32_t ts = sa; sa = sb; sb = ts;
+    }
+    u128 A = (u128)ma << 64, B = (u128)mb << 64;
+    const int d = xa - xb;
+    if (d >= 128) {
+        B = B != 0;
+    } else if (d > 0) {
+        const bool sticky = (B << (128 - d)) != 0;
+        B = (B >> d) | (u128)sticky;
+    }
+    int e = xa;
+    u128 S;
+    if (sa == sb) {
+        S = A + B;
+        if (S < A) {                                  // carry out of bit 127
+            S = (S >> 1) | (S & 1) | ((u128)1 << 127);
+            ++e;
+        }
+    } else {
+        S = A - B;
+        if (S == 0) return with_bits(a, 0, 0);        // exact cancellation: +0
+        int lz = clz128(S);
+        if (lz > e - 1) lz = e - 1;
+        S <<= lz;
+        e -= lz;
+    }
+    return round_pack(a, sa, e, S);
+}
+
+// a * b (the reference's `a[i] = a[i] * b[i]`); pads from a
+XF_FN xf80 mul(xf80 a, xf80 b)
+{
+    const uint32_t ea = a.se & 0x7fff, eb = b.se & 0x7fff;
+    const uint32_t s = (a.se ^ b.se) >> 15;
+    const int ka = klass(a.m, ea), kb = klass(b.m, eb);
+    if (ka == K_BAD || kb == K_BAD) return indefinite(a);
+    if (ka >= K_QNAN || kb >= K_QNAN) return nan_result(a, ka, b, kb);
+    if (ka == K_INF || kb == K_INF) {
+        if (ka == K_ZERO || kb == K_ZERO) return indefinite(a);
+        return with_bits(a, 1ull << 63, (s << 15) | 0x7fff);
+    }
+    if (ka == K_ZERO || kb == K_ZERO) return with_bits(a, 0, s << 15);
+    int xa = ea ? (int)ea : 1, xb = eb ? (int)eb : 1;
+    uint64_t ma = a.m, mb = b.m;
+    int la = __builtin_clzll(ma), lb = __builtin_clzll(mb);
+    ma <<= la;
+    mb <<= lb;
+    xa -= la;
+    xb -= lb;
+    u128 P = (u128)ma * mb;                           // in [2^126, 2^128)
+    int e = xa + xb - 16383 + 1;
+    if (!(P >> 127)) {
+        P <<= 1;
+        --e;
+    }
+    if (e < 1) {                                      // denormalise, then one rounding
+        const int sh = 1 - e;
+        if (sh >= 128) {
+            P = P != 0;
+        } else {
+            const bool sticky = (P << (128 - sh)) != 0;
+            P = (P >> sh) | (u128)sticky;
+        }
+        e = 1;
+    }
+    return round_pack(a, s, e, P);
+}
+
+// x87 compare: -1, 0, 1, or 2 = unordered (NaN or invalid encoding)
+XF_FN int cmp(const xf80 &a, const xf80 &b)
+{
+    const uint32_t ea = a.se & 0x7fff, eb = b.se & 0x7fff;
+    const int ka = klass(a.m, ea), kb = klass(b.m, eb);
+    if (ka >= K_QNAN || kb >= K_QNAN) return 2;
+    if (ka == K_ZERO && kb == K_ZERO) return 0;
+    const uint32_t sa = a.se >> 15, sb = b.se >> 15;
+    if (sa != sb) return sa ? -1 : 1;
+    const u128 A = ka == K_ZERO ? 0 : ((u128)(ea ? ea : 1) << 64) | a.m;
+    const u128 B = kb == K_ZERO ? 0 : ((u128)(eb ? eb : 1) << 64) | b.m;
+    const int c = A == B ? 0 : (A < B ? -1 : 1);
+    return sa ? -c : c;
+}
+
+XF_FN bool truth(const xf80 &a)                       // `a != 0`, unordered is true
+{
+    const int k = klass(a.m, a.se & 0x7fff);
+    return k != K_ZERO;
+}
+
+XF_FN xf80 from_bool(xf80 pads, bool t)               // (long double)(int)t
+{
+    return t ? with_bits(pads, 1ull << 63, 0x3fff) : with_bits(pads, 0, 0);
+}
+
+// the reference's MPI_MAX / MPI_MIN select (coll.h:14-19): the chosen
+// operand's 10 value bytes, the slot padding of a
+XF_FN xf80 max(xf80 a, xf80 b) { return cmp(b, a) == 1 ? with_bits(a, b.m, b.se) : a; }
+XF_FN xf80 min(xf80 a, xf80 b) { return cmp(a, b) == 1 ? with_bits(a, b.m, b.se) : a; }
+
+XF_FN xf80 land(xf80 a, xf80 b) { return from_bool(a, truth(a) && truth(b)); }
+XF_FN xf80 lor(xf80 a, xf80 b) { return from_bool(a, truth(a) || truth(b)); }
+XF_FN xf80 lxor(xf80 a, xf80 b) { return from_bool(a, truth(a) != truth(b)); }
+
+// MPI_LONG_DOUBLE_INT: struct { long double value; int loc; } (global_ops.c
+// 1263-1268), 32 bytes; the padding after loc is an explicit member
+struct pxi {
+    xf80 v;
+    int32_t l;
+    int32_t pad[3];
+};
+
+// global_ops.c:1365-1378 (MAXLOC) and 1605-1618 (MINLOC): equal values keep
+// the smaller loc; otherwise b replaces a only when strictly larger
+// (smaller), value bytes and loc; unordered keeps a
+template <bool MIN>
+XF_FN pxi loc(pxi a, pxi b)
+{
+    const int c = cmp(a.v, b.v);
+    pxi r = a;
+    if (c == 0) {
+        r.l = a.l < b.l ? a.l : b.l;
+    } else if (c == (MIN ? 1 : -1)) {
+        r.v = with_bits(a.v, b.v.m, b.v.se);
+        r.l = b.l;
+    }
+    return r;
+}
+
+}  // namespace xf

@@ -39,17 +39,14 @@ def test_libraries_are_in_tree(mvx):
 
 def test_op_support_matrix_matches_reference(mvx, oracle):
     """mvx_op_supported / mvx_op_apply's verdict == global_ops.c's switch
-    (SURVEY.md Appendix B); x87 long double has no device representation."""
+    (SURVEY.md Appendix B), the x87 long double types included."""
     for op in range(100, 112):
         for dtype in T.ALL_TYPES:
             ref = T.oracle_rc(oracle, op, dtype)
             verdict = mvx.hip().mvx_op_apply(op, dtype, None, None, 0, None)
-            if dtype in (12, 22):
-                assert verdict == (3 if ref == 0 else ref)
-                assert not mvx.hip().mvx_op_supported(op, dtype)
-            else:
-                assert verdict == ref, (op, dtype)
-                assert bool(mvx.hip().mvx_op_supported(op, dtype)) == (ref == 0)
+            assert verdict == ref, (op, dtype)
+            assert bool(mvx.hip().mvx_op_supported(op, dtype)) == (ref == 0)
+            assert (dtype in mvx.DEFINED[op]) == (ref == 0), (op, dtype)
     assert mvx.hip().mvx_op_apply(99, 10, None, None, 0, None) == mvx.MPI_ERR_OP
 
 
@@ -58,8 +55,8 @@ def test_dtype_extents(mvx, oracle):
         e, s = mvx.dtype_info(dtype)
         oe, os_ = oracle.dtype_info(dtype)
         assert (e, s) == (oe, os_), dtype
-        if dtype not in (12, 22):
-            assert mvx.hip().mvx_dtype_extent(dtype) == e
+        assert mvx.hip().mvx_dtype_extent(dtype) == e
+        assert mvx.NP_DTYPE[dtype].itemsize == e
 
 
 def test_op_create_free_semantics(mvx):

@@ -13,7 +13,8 @@ from plan_exec import run_plans
 import mvxtest as T
 
 CASES = [(102, 10), (100, 10), (101, 10), (101, 11), (103, 11), (111, 17), (110, 17), (110, 18), (111, 19),
-         (111, 20), (110, 21), (105, 8), (108, 4), (102, 6), (102, 23), (103, 24), (109, 3)]
+         (111, 20), (110, 21), (105, 8), (108, 4), (102, 6), (102, 23), (103, 24), (109, 3),
+         (102, 12), (103, 12), (100, 12), (104, 12), (111, 22), (110, 22)]
 
 
 def special_vec(dtype, n, seed):

@@ -15,7 +15,7 @@ import mvxtest as T
 pytestmark = pytest.mark.gpu
 
 CASES = [(102, 10), (100, 10), (101, 11), (111, 17), (110, 18), (105, 8), (103, 6), (108, 4), (111, 20),
-         (110, 21), (102, 24), (109, 3)]
+         (110, 21), (102, 24), (109, 3), (102, 12), (100, 12), (111, 22)]
 SIZES = [1, 7, 10, 1000, 2047, 2048, 4097, 16385, 70001, 140001]
 
 

@@ -34,6 +34,8 @@ def run(mvx, name, op, dtype, k, shape, leaf_bytes, sets, reps=20, warm=3):
         leaves = [torch.randint(0, 1 << 30, (leaf_bytes // 4,), dtype=torch.int32, device="cuda") for _ in range(k)]
         if dtype == mvx.MPI_FLOAT:
             leaves = [(x.float() * 1e-6) for x in leaves]
+        elif dtype in (mvx.MPI_LONG_DOUBLE, mvx.MPI_LONG_DOUBLE_INT):
+            leaves = [_x87_values(x, dtype, mvx) for x in leaves]
         dst = torch.empty(leaf_bytes // 4, dtype=torch.int32, device="cuda")
         bufs.append((leaves, dst))
     stream = torch.cuda.current_stream()
@@ -67,12 +69,28 @@ def run(mvx, name, op, dtype, k, shape, leaf_bytes, sets, reps=20, warm=3):
     return out
 
 
+def _x87_values(x, dtype, mvx):
+    """Finite x87 values near 1 (normal operands: the emulation's main path)."""
+    import torch
+    w = x.view(torch.int64).view(-1, 2 if dtype == mvx.MPI_LONG_DOUBLE else 4)
+    w[:, 0] |= torch.iinfo(torch.int64).min                       # integer bit
+    w[:, 1] = 16383 + (w[:, 1] & 15) - 8 + ((w[:, 1] >> 8) & 1) * 0x8000
+    return x
+
+
 def main():
     mvx = importlib.import_module("mvapich-cce_amd")
     run(mvx, "C2", mvx.MPI_SUM, mvx.MPI_FLOAT, 2, 1, 256 * MIB, 4)
     run(mvx, "C3", mvx.MPI_SUM, mvx.MPI_FLOAT, 8, 0, 32 * MIB, 4)
     run(mvx, "C4", mvx.MPI_BAND, mvx.MPI_LONG, 4, 1, 256 * MIB, 2)
     run(mvx, "C5", mvx.MPI_MAXLOC, mvx.MPI_FLOAT_INT, 8, 0, 64 * MIB, 2)
+    if "x87" in sys.argv[1:]:
+        # x87 long double (integer emulation): apply and the C3 / C5 shapes
+        run(mvx, "X2-sum", mvx.MPI_SUM, mvx.MPI_LONG_DOUBLE, 2, 1, 256 * MIB, 4)
+        run(mvx, "X2-prod", mvx.MPI_PROD, mvx.MPI_LONG_DOUBLE, 2, 1, 256 * MIB, 4)
+        run(mvx, "X2-max", mvx.MPI_MAX, mvx.MPI_LONG_DOUBLE, 2, 1, 256 * MIB, 4)
+        run(mvx, "X3-sum", mvx.MPI_SUM, mvx.MPI_LONG_DOUBLE, 8, 0, 32 * MIB, 4)
+        run(mvx, "X5-maxloc", mvx.MPI_MAXLOC, mvx.MPI_LONG_DOUBLE_INT, 8, 0, 64 * MIB, 2)
 
 
 if __name__ == "__main__":

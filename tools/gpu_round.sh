@@ -37,6 +37,10 @@ if [[ $STAGE == all || $STAGE == host ]]; then
   run timeout -k 10 300 python tools/bench_host.py > gpurun_out/bench_host.jsonl 2> gpurun_out/bench_host.err || { tail -20 gpurun_out/bench_host.err; exit 1; }
   cat gpurun_out/bench_host.jsonl
 fi
+if [[ $STAGE == x87 ]]; then
+  run timeout -k 10 300 python tools/bench_kernels.py x87 > gpurun_out/bench_kernels_x87.jsonl 2> gpurun_out/bench_kernels.err || { tail -20 gpurun_out/bench_kernels.err; exit 1; }
+  cat gpurun_out/bench_kernels_x87.jsonl
+fi
 if [[ $STAGE == kernels_ab ]]; then
   run timeout -k 10 300 python tools/bench_kernels.py > gpurun_out/bench_kernels_u2.jsonl 2> gpurun_out/bench_kernels.err || exit 1
   MVX_PROG_U1=1 run timeout -k 10 300 python tools/bench_kernels.py > gpurun_out/bench_kernels_u1.jsonl 2>> gpurun_out/bench_kernels.err || exit 1
