@@ -61,6 +61,16 @@ int MPI_Scan(void *sendbuf, void *recvbuf, int count, MPI_Datatype datatype,
              MPI_Op op, MPI_Comm comm);
 int MPI_Op_create(MPI_User_function *function, int commute, MPI_Op *op);
 int MPI_Op_free(MPI_Op *op);
+
+/* A user op whose function runs on the device: `function` enqueues
+ * inoutvec[i] = invec[i] op inoutvec[i], i < len, on `stream` (a
+ * hipStream_t) and returns 0, or nonzero to fail the call.  Collectives give
+ * it the same operand roles and order as an MPI_Op_create op with the same
+ * commute flag; no data leaves HBM.  (Extension: the reference has host
+ * functions only.) */
+typedef int (MVX_Device_function)(const void *invec, void *inoutvec, size_t len,
+                                  MPI_Datatype datatype, void *stream);
+int mvx_op_create_device(MVX_Device_function *function, int commute, MPI_Op *op);
 int MPI_Error_class(int errorcode, int *errorclass);
 
 /* The same three calls under names that cannot collide with a host MPI
@@ -159,6 +169,13 @@ int mvx_op_errno(void);
 #define MVX_ALG_RS_HALVING    4
 #define MVX_ALG_RS_PAIRWISE   5
 #define MVX_ALG_SCAN_RECDBL   6
+#define MVX_ALG_RS_RECDBL     7   /* noncommutative Reduce_scatter < 512 bytes */
+
+/* What kind of op a plan is for: the reference's struct MPIR_OP
+ * {permanent, commute} (include/mpiops.h:1-11) */
+#define MVX_OPKIND_PREDEFINED      0   /* permanent, commutative          */
+#define MVX_OPKIND_USER_COMMUTE    1   /* MPI_Op_create(f, 1, ...)        */
+#define MVX_OPKIND_USER_NONCOMMUTE 2   /* MPI_Op_create(f, 0, ...)        */
 
 typedef struct { long off, cnt; } mvx_range;   /* in elements */
 
@@ -184,13 +201,25 @@ typedef struct mvx_plan {
     long c_src_off, c_cnt, c_dst_off;
     mvx_range b_send[MVX_MAXP];
     mvx_range b_recv[MVX_MAXP];
+    int opkind;                       /* MVX_OPKIND_* */
+    /* steps whose operand roles are exchanged: bit set -> the step is
+     * y = uop(in = y_left, inout = y_right), the reference's noncommutative
+     * "order is not right" branch; bits as in tree_mask / chain_mask.  Only
+     * user ops set them (the device kernels never see a swap). */
+    unsigned tree_swap, chain_swap;
 } mvx_plan;
 
 /* Builds rank `rank`'s plan; returns 0 or an MPI error class. */
 int mvx_plan_build(mvx_plan *plan, int coll, int p, int rank, long count,
                    const int *recvcnts, int dtype, int op, int root);
-/* The reference's algorithm for (coll, p, total elements, dtype). */
+/* The same for a user op (opkind MVX_OPKIND_*): permanent == 0 forces
+ * recursive doubling / the binomial tree (intra_fns_new.c:5590, 4620), and a
+ * noncommutative op takes the reference's order-preserving branches. */
+int mvx_plan_build_kind(mvx_plan *plan, int coll, int p, int rank, long count,
+                        const int *recvcnts, int dtype, int op, int root, int opkind);
+/* The reference's algorithm for (coll, p, total elements, dtype[, opkind]). */
 int mvx_plan_algorithm(int coll, int p, long total_count, int dtype);
+int mvx_plan_algorithm_kind(int coll, int p, long total_count, int dtype, int opkind);
 /* Datatype facts: extent and MPI_Type_size; returns 0 or MPI_ERR_TYPE. */
 int mvx_dtype_info(int dtype, int *extent, int *type_size);
 

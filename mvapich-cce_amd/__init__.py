@@ -63,6 +63,7 @@ class Plan(ctypes.Structure):
         ("leaf", ctypes.c_int * MAXK), ("leaf_fold", ctypes.c_int * MAXK),
         ("c_src_off", ctypes.c_long), ("c_cnt", ctypes.c_long), ("c_dst_off", ctypes.c_long),
         ("b_send", Range * MAXP), ("b_recv", Range * MAXP),
+        ("opkind", ctypes.c_int), ("tree_swap", ctypes.c_uint), ("chain_swap", ctypes.c_uint),
     ]
 
 
@@ -117,6 +118,7 @@ def _load():
     for name in ("MPI_Reduce_scatter", "PMPI_Reduce_scatter", "mvx_coll_reduce_scatter"):
         getattr(c, name).argtypes = [vp, vp, pi, i, i, i]
     c.MPI_Op_create.argtypes = [vp, i, pi]
+    c.mvx_op_create_device.argtypes = [vp, i, pi]
     c.MPI_Op_free.argtypes = [pi]
     c.MPI_Error_class.argtypes = [i, pi]
     c.mvx_allreduce_async.argtypes = [vp, vp, i, i, i, i, vp]
@@ -127,6 +129,8 @@ def _load():
     c.mvx_reduce_scatter_multi.argtypes = [pvp, pvp, pi, i, i, i, pi, vp]
     c.mvx_plan_build.argtypes = [ctypes.POINTER(Plan), i, i, i, ctypes.c_long, pi, i, i, i]
     c.mvx_plan_algorithm.argtypes = [i, i, ctypes.c_long, i]
+    c.mvx_plan_build_kind.argtypes = [ctypes.POINTER(Plan), i, i, i, ctypes.c_long, pi, i, i, i, i]
+    c.mvx_plan_algorithm_kind.argtypes = [i, i, ctypes.c_long, i, i]
     c.mvx_dtype_info.argtypes = [i, pi, pi]
     for name in ("MPIR_MAXF", "MPIR_MINF", "MPIR_SUM", "MPIR_PROD", "MPIR_LAND", "MPIR_BAND", "MPIR_LOR",
                  "MPIR_BOR", "MPIR_LXOR", "MPIR_BXOR", "MPIR_MAXLOC", "MPIR_MINLOC"):
@@ -153,19 +157,26 @@ def loaded_paths():
 
 # ---------------------------------------------------------------- plans ----
 
-def plan(coll_kind, p, rank, count, dtype, op, root=0, recvcnts=None):
+def plan(coll_kind, p, rank, count, dtype, op, root=0, recvcnts=None, opkind=None):
+    """Rank `rank`'s plan; opkind (OPKIND_*) for a user op, None = predefined."""
     P = Plan()
     rc_arr = None
     if recvcnts is not None:
         rc_arr = (ctypes.c_int * p)(*recvcnts)
-    rc = coll().mvx_plan_build(ctypes.byref(P), coll_kind, p, rank, count, rc_arr, dtype, op, root)
+    if opkind is None:
+        rc = coll().mvx_plan_build(ctypes.byref(P), coll_kind, p, rank, count, rc_arr, dtype, op, root)
+    else:
+        rc = coll().mvx_plan_build_kind(ctypes.byref(P), coll_kind, p, rank, count, rc_arr, dtype, op, root,
+                                        opkind)
     if rc:
         raise ValueError("mvx_plan_build rc=%d" % rc)
     return P
 
 
-def algorithm(coll_kind, p, total, dtype):
-    return coll().mvx_plan_algorithm(coll_kind, p, total, dtype)
+def algorithm(coll_kind, p, total, dtype, opkind=None):
+    if opkind is None:
+        return coll().mvx_plan_algorithm(coll_kind, p, total, dtype)
+    return coll().mvx_plan_algorithm_kind(coll_kind, p, total, dtype, opkind)
 
 
 def dtype_info(dtype):

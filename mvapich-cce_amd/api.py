@@ -11,7 +11,7 @@ from .consts import COLL_ALLREDUCE, COLL_REDUCE, COLL_REDUCE_SCATTER  # noqa: F4
 
 __all__ = [
     "addr", "stream_handle", "op_apply", "op_combine", "op_program", "Comm",
-    "MPI_Allreduce", "MPI_Reduce", "MPI_Reduce_scatter", "MPI_Scan", "MPI_Op_create", "MPI_Op_free",
+    "MPI_Allreduce", "MPI_Reduce", "MPI_Reduce_scatter", "MPI_Scan", "MPI_Op_create", "MPI_Op_free", "op_create_device",
     "MPIR_call", "op_errno", "last_kernel", "set_launch",
 ]
 
@@ -197,11 +197,26 @@ _keepalive = []
 
 
 def MPI_Op_create(function, commute):
-    """Returns (rc, op_handle); `function(invec, inoutvec, len_ptr, type_ptr)`."""
-    cb = _USER_FN(function)
-    _keepalive.append(cb)
+    """Returns (rc, op_handle).  `function` is a C MPI_User_function address
+    (int) or a Python callable `function(invec, inoutvec, len_ptr, type_ptr)`."""
+    if isinstance(function, int):
+        fp = ctypes.c_void_p(function)
+    else:
+        cb = _USER_FN(function)
+        _keepalive.append(cb)
+        fp = ctypes.cast(cb, ctypes.c_void_p)
     h = ctypes.c_int()
-    rc = coll().MPI_Op_create(ctypes.cast(cb, ctypes.c_void_p), commute, ctypes.byref(h))
+    rc = coll().MPI_Op_create(fp, commute, ctypes.byref(h))
+    return rc, h.value
+
+
+def op_create_device(function_addr, commute):
+    """mvx_op_create_device: `function_addr` is the address of a C
+    MVX_Device_function (int (*)(const void *in, void *inout, size_t len,
+    MPI_Datatype, void *stream)) that enqueues the op on `stream`.
+    Returns (rc, op_handle)."""
+    h = ctypes.c_int()
+    rc = coll().mvx_op_create_device(ctypes.c_void_p(function_addr), commute, ctypes.byref(h))
     return rc, h.value
 
 

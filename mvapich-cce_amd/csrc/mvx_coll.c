@@ -63,6 +63,10 @@ typedef struct {
     size_t pool_bytes;
     char *hpool;         /* host-buffer staging */
     size_t hpool_bytes;
+    char *upool;         /* user-op scratch: device (device functions) */
+    size_t upool_bytes;
+    char *uhost;         /* user-op scratch: pinned host (MPI_User_functions) */
+    size_t uhost_bytes;
 } mvx_comm_t;
 
 static mvx_comm_t g_comms[MAX_COMMS];
@@ -137,6 +141,8 @@ int mvx_comm_free(MPI_Comm *comm)
     if (c->nccl) ncclCommDestroy(c->nccl);
     if (c->pool) hipFree(c->pool);
     if (c->hpool) hipFree(c->hpool);
+    if (c->upool) hipFree(c->upool);
+    if (c->uhost) hipHostFree(c->uhost);
     if (c->handle == MPI_COMM_WORLD) g_have_world = 0;
     memset(c, 0, sizeof *c);
     *comm = 0;
@@ -177,6 +183,16 @@ static int grow(char **buf, size_t *have, size_t need)
     return MPI_SUCCESS;
 }
 
+static int grow_host(char **buf, size_t *have, size_t need)
+{
+    if (need <= *have) return MPI_SUCCESS;
+    if (*buf) { hipHostFree(*buf); *buf = NULL; *have = 0; }
+    need = (need + (1 << 20) - 1) & ~(size_t)((1 << 20) - 1);
+    if (hipHostMalloc((void **)buf, need, hipHostMallocDefault) != hipSuccess) { *buf = NULL; return MPI_ERR_OTHER; }
+    *have = need;
+    return MPI_SUCCESS;
+}
+
 int mvx_comm_reserve(MPI_Comm comm, size_t bytes)
 {
     mvx_comm_t *c = get_comm(comm);
@@ -190,7 +206,8 @@ int mvx_comm_reserve(MPI_Comm comm, size_t bytes)
 #define MAX_USER_OPS 64
 #define USER_OP_BASE 200
 typedef struct {           /* struct MPIR_OP, include/mpiops.h:1-11 */
-    MPI_User_function *op;
+    MPI_User_function *op;     /* host function (MPI_Op_create) */
+    MVX_Device_function *dop;  /* stream-ordered device function */
     unsigned cookie;
     int commute, permanent;
 } mvx_op_t;
@@ -206,12 +223,14 @@ static mvx_op_t *user_op(MPI_Op op)
     return &g_user_ops[i];
 }
 
-int MPI_Op_create(MPI_User_function *function, int commute, MPI_Op *op)
+static int op_register(MPI_User_function *fn, MVX_Device_function *dfn, int commute, MPI_Op *op)
 {
     int i;
+    if (!op) return MPI_ERR_ARG;
     for (i = 0; i < MAX_USER_OPS; i++) {
         if (g_user_ops[i].cookie != OP_COOKIE) {
-            g_user_ops[i].op = function;
+            g_user_ops[i].op = fn;
+            g_user_ops[i].dop = dfn;
             g_user_ops[i].cookie = OP_COOKIE;
             g_user_ops[i].commute = commute;
             g_user_ops[i].permanent = 0;
@@ -220,6 +239,26 @@ int MPI_Op_create(MPI_User_function *function, int commute, MPI_Op *op)
         }
     }
     return MPI_ERR_INTERN;
+}
+
+int MPI_Op_create(MPI_User_function *function, int commute, MPI_Op *op)
+{
+    return op_register(function, NULL, commute, op);
+}
+
+int mvx_op_create_device(MVX_Device_function *function, int commute, MPI_Op *op)
+{
+    if (!function) return MPI_ERR_ARG;
+    return op_register(NULL, function, commute, op);
+}
+
+/* the plan kind of an op handle (an invalid handle plans as predefined and
+ * is rejected by op_verdict) */
+static int op_kind(MPI_Op op)
+{
+    const mvx_op_t *o = predefined(op) ? NULL : user_op(op);
+    if (!o) return MVX_OPKIND_PREDEFINED;
+    return o->commute ? MVX_OPKIND_USER_COMMUTE : MVX_OPKIND_USER_NONCOMMUTE;
 }
 
 int MPI_Op_free(MPI_Op *op)  /* opfree.c:51-82 */
@@ -236,12 +275,12 @@ int MPI_Op_free(MPI_Op *op)  /* opfree.c:51-82 */
 }
 
 /* The op's verdict on (op, type) before any data moves: 0, 329 (undefined
- * pair, reported only by ranks that call the op), MPI_ERR_TYPE (no device
- * representation), MPI_ERR_OP (bad handle; user ops have no device path). */
+ * pair, reported only by ranks that call the op), MPI_ERR_OP (bad handle).
+ * A user function accepts every datatype (the reference never checks). */
 static int op_verdict(MPI_Op op, MPI_Datatype dt)
 {
-    if (!predefined(op)) return MPI_ERR_OP;
-    return mvx_op_apply(op, dt, NULL, NULL, 0, NULL);
+    if (predefined(op)) return mvx_op_apply(op, dt, NULL, NULL, 0, NULL);
+    return user_op(op) ? MPI_SUCCESS : MPI_ERR_OP;
 }
 
 /* ---------------------------------------------------------------------- */
@@ -268,7 +307,83 @@ static size_t slot_at(size_t cur, const void *like)
 
 #define NCCL_OK(x) do { if ((x) != ncclSuccess) return MPI_ERR_OTHER; } while (0)
 
-static int combine(const mvx_plan *P, const char *const *leafp, void *dst,
+/* ---- user ops: the combine program as a sequence of user calls --------
+ * The reference hands a user function (*uop)(in, inout, &len, &type) its
+ * operands in the roles the plan's program records, a swapped step being
+ * uop(in = left, inout = right) whose result becomes the left value.  The
+ * program runs over k scratch copies of the leaves (a user function writes
+ * its inout operand, and leaves include the caller's send buffer); a swap
+ * just renames which scratch buffer holds the left value. */
+static int call_host(const mvx_op_t *o, const char *in, char *inout, long n, int esize,
+                     MPI_Datatype dt)
+{
+    while (n > 0) {   /* the reference's len is an int */
+        int len = n > 0x40000000L ? 0x40000000 : (int)n;
+        MPI_Datatype t = dt;
+        o->op((void *)in, inout, &len, &t);
+        in += (long)len * esize;
+        inout += (long)len * esize;
+        n -= len;
+    }
+    return MPI_SUCCESS;
+}
+
+static int user_step(const mvx_op_t *o, const char *in, char *inout, long n, int esize,
+                     MPI_Datatype dt, hipStream_t st)
+{
+    if (o->dop) return o->dop(in, inout, (size_t)n, dt, st) ? MPI_ERR_OTHER : MPI_SUCCESS;
+    return call_host(o, in, inout, n, esize, dt);
+}
+
+static int combine_user(mvx_comm_t *c, const mvx_plan *P, const void *const *srcs,
+                        const void *const *fold, void *dst, hipStream_t st)
+{
+    const mvx_op_t *o = user_op(P->op);
+    const long n = P->c_cnt, E = P->esize;
+    const size_t bytes = (size_t)(n * E), slot = (bytes + 255) & ~(size_t)255;
+    const int dev = o && o->dop;
+    const hipMemcpyKind in_kind = dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+    char *y[MVX_COMBINE_KMAX], *base;
+    int q, l, rc;
+    if (!o) return MPI_ERR_OP;
+    if (dev) rc = grow(&c->upool, &c->upool_bytes, slot * (size_t)P->k * 2);
+    else rc = grow_host(&c->uhost, &c->uhost_bytes, slot * (size_t)P->k * 2);
+    if (rc) return rc;
+    base = dev ? c->upool : c->uhost;
+    for (q = 0; q < P->k; q++) {
+        y[q] = base + slot * (size_t)q;
+        if (hipMemcpyAsync(y[q], srcs[q], bytes, in_kind, st) != hipSuccess) return MPI_ERR_OTHER;
+        if (fold[q] && hipMemcpyAsync(base + slot * (size_t)(P->k + q), fold[q], bytes, in_kind, st) != hipSuccess)
+            return MPI_ERR_OTHER;
+    }
+    if (!dev && hipStreamSynchronize(st) != hipSuccess) return MPI_ERR_OTHER;
+    for (q = 0; q < P->k; q++)   /* leaf q = op(leaf, fold): fold is `in` */
+        if (fold[q] && (rc = user_step(o, base + slot * (size_t)(P->k + q), y[q], n, (int)E, P->dtype, st)))
+            return rc;
+    for (l = 0; l < 3; l++)
+        for (q = 0; q + (1 << l) < P->k; q++) {
+            const unsigned bit = 1u << (l * 8 + q);
+            char *a = y[q], *b = y[q + (1 << l)];
+            if (!(P->tree_mask & bit)) continue;
+            if (P->tree_swap & bit) { rc = user_step(o, a, b, n, (int)E, P->dtype, st); y[q] = b; y[q + (1 << l)] = a; }
+            else rc = user_step(o, b, a, n, (int)E, P->dtype, st);
+            if (rc) return rc;
+        }
+    for (q = 1; q < P->k; q++) {
+        const unsigned bit = 1u << q;
+        char *a = y[0], *b = y[q];
+        if (!(P->chain_mask & bit)) continue;
+        if (P->chain_swap & bit) { rc = user_step(o, a, b, n, (int)E, P->dtype, st); y[0] = b; y[q] = a; }
+        else rc = user_step(o, b, a, n, (int)E, P->dtype, st);
+        if (rc) return rc;
+    }
+    if (hipMemcpyAsync(dst, y[0], bytes, dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, st) != hipSuccess)
+        return MPI_ERR_OTHER;
+    /* the pinned scratch is reused by the next call */
+    return (!dev && hipStreamSynchronize(st) != hipSuccess) ? MPI_ERR_OTHER : MPI_SUCCESS;
+}
+
+static int combine(mvx_comm_t *c, const mvx_plan *P, const char *const *leafp, void *dst,
                    hipStream_t st)
 {
     const void *srcs[MVX_COMBINE_KMAX], *fold[MVX_COMBINE_KMAX];
@@ -278,6 +393,7 @@ static int combine(const mvx_plan *P, const char *const *leafp, void *dst,
         srcs[q] = leafp[P->leaf[q]];
         fold[q] = P->leaf_fold[q] >= 0 ? leafp[P->leaf_fold[q]] : NULL;
     }
+    if (P->opkind != MVX_OPKIND_PREDEFINED) return combine_user(c, P, srcs, fold, dst, st);
     return mvx_op_program(P->op, P->dtype, srcs, fold, P->k, P->tree_mask,
                           P->chain_mask, dst, (size_t)P->c_cnt, st);
 }
@@ -352,6 +468,7 @@ static int lb_flush(loopback_t *lb, hipStream_t st)
 /* ---- one rank's execution of its plan ---------------------------------- */
 typedef struct {
     const mvx_plan *P;
+    mvx_comm_t *c;
     const char *sendbuf;
     char *recvbuf;
     char *pool;                     /* this rank's staging region */
@@ -411,7 +528,7 @@ static int exec_phase_b(rank_exec_t *X, hipStream_t st)
     if (!P->has_combine || P->c_cnt == 0) return MPI_SUCCESS;
     for (s = 0; s < P->p; s++)
         leafp[s] = (s == P->rank) ? X->sendbuf + P->c_src_off * E : X->pool + X->slot[s];
-    return combine(P, leafp, exec_out(X), st);
+    return combine(X->c, P, leafp, exec_out(X), st);
 }
 
 /* phase C: combined blocks to the ranks that need them */
@@ -443,7 +560,7 @@ static int exec_plan(mvx_comm_t *c, const mvx_plan *P, const char *sendbuf,
     memset(&t, 0, sizeof t);
     t.start = nc_start; t.end = nc_end; t.send = nc_send; t.recv = nc_recv;
     t.nccl = c->nccl; t.me = c->rank;
-    X.P = P; X.sendbuf = sendbuf; X.recvbuf = recvbuf;
+    X.P = P; X.c = c; X.sendbuf = sendbuf; X.recvbuf = recvbuf;
     if ((rc = grow(&c->pool, &c->pool_bytes, exec_layout(&X)))) return rc;
     X.pool = c->pool;
     if ((rc = exec_phase_a(&X, &t, st))) return rc;
@@ -489,8 +606,8 @@ static int run(mvx_comm_t *c, const call_t *k, hipStream_t st, int blocking)
 
     if (c->local) return MPI_ERR_COMM;   /* virtual comms use *_multi */
     mvx_dtype_info(k->dt, &e, &ts);
-    rc = mvx_plan_build(&P, k->coll, c->size, c->rank, k->count, k->recvcnts,
-                        k->dt, k->op, k->root);
+    rc = mvx_plan_build_kind(&P, k->coll, c->size, c->rank, k->count, k->recvcnts,
+                             k->dt, k->op, k->root, op_kind(k->op));
     if (rc) return rc;
     if (P.alg == MVX_ALG_NONE) return MPI_SUCCESS;
     verdict = op_verdict(k->op, k->dt);
@@ -711,7 +828,7 @@ static int run_multi(mvx_comm_t *c, int coll, void *const *sendbufs,
     for (r = 0; r < p; r++) rcs[r] = 0;
     if (!predefined(op) && !user_op(op)) { for (r = 0; r < p; r++) rcs[r] = MPI_ERR_OP; return MPI_SUCCESS; }
     for (r = 0; r < p; r++) {
-        rc = mvx_plan_build(&plans[r], coll, p, r, count, recvcnts, dt, op, root);
+        rc = mvx_plan_build_kind(&plans[r], coll, p, r, count, recvcnts, dt, op, root, op_kind(op));
         if (rc) return rc;
     }
     if (plans[0].alg == MVX_ALG_NONE) return MPI_SUCCESS;
@@ -733,6 +850,7 @@ static int run_multi(mvx_comm_t *c, int coll, void *const *sendbufs,
             return MPI_ERR_BUFFER;
         if (sendbufs[r] == recvbufs[r]) return MPI_ERR_BUFFER;
         X[r].P = &plans[r];
+        X[r].c = c;
         X[r].sendbuf = (const char *)sendbufs[r];
         X[r].recvbuf = (char *)recvbufs[r];
         base[r] = (need + 255) & ~(size_t)255;

@@ -44,7 +44,8 @@ static const int coll_table_flat[3 * 5] = {
     -1, 65536, 4096, 4096, 4096 };
 #define ALLREDUCE_IDX 1
 #define REDUCE_IDX 2
-#define REDSCAT_COMMUTATIVE_LONG_MSG 524288   /* intra_fns_new.c:39 */
+#define REDSCAT_COMMUTATIVE_LONG_MSG 524288   /* intra_fns_new.c:39-40 */
+#define REDSCAT_NONCOMMUTATIVE_SHORT_MSG 512
 
 int mvx_dtype_info(int dtype, int *extent, int *type_size)
 {
@@ -104,28 +105,38 @@ static int imul32(long a, long b)
     return (int)(unsigned int)((unsigned long)a * (unsigned long)b);
 }
 
-int mvx_plan_algorithm(int coll, int p, long total, int dtype)
+int mvx_plan_algorithm_kind(int coll, int p, long total, int dtype, int kind)
 {
     int e, ts, lgn, pof2, tv;
+    const int permanent = kind == MVX_OPKIND_PREDEFINED;
+    const int commute = kind != MVX_OPKIND_USER_NONCOMMUTE;
     if (mvx_dtype_info(dtype, &e, &ts) || p < 1 || total <= 0) return MVX_ALG_NONE;
     pof2 = pof2_lgn(p, &lgn);
     switch (coll) {
     case MVX_COLL_ALLREDUCE:     /* intra_fns_new.c:5589-5591 */
         tv = coll_table_flat[ALLREDUCE_IDX * 5 + lgn];
-        if (tv == -1 || imul32(total, ts) < tv || total < pof2) return MVX_ALG_RECDBL;
+        if (tv == -1 || imul32(total, ts) < tv || !permanent || total < pof2)
+            return MVX_ALG_RECDBL;
         return MVX_ALG_RABENSEIFNER;
     case MVX_COLL_REDUCE:        /* intra_fns_new.c:4619-4620 */
         tv = coll_table_flat[REDUCE_IDX * 5 + lgn];
-        if (tv != -1 && imul32(total, ts) > tv && total >= pof2) return MVX_ALG_RABENSEIFNER;
+        if (tv != -1 && imul32(total, ts) > tv && permanent && total >= pof2)
+            return MVX_ALG_RABENSEIFNER;
         return MVX_ALG_BINOMIAL;
-    case MVX_COLL_REDUCE_SCATTER: /* intra_fns_new.c:6248, 6450 (commutative) */
-        return imul32(total, ts) < REDSCAT_COMMUTATIVE_LONG_MSG ? MVX_ALG_RS_HALVING
-                                                                : MVX_ALG_RS_PAIRWISE;
+    case MVX_COLL_REDUCE_SCATTER: /* intra_fns_new.c:6248, 6450-6452, 6505 */
+        if (commute && imul32(total, ts) < REDSCAT_COMMUTATIVE_LONG_MSG) return MVX_ALG_RS_HALVING;
+        if (!commute && imul32(total, ts) < REDSCAT_NONCOMMUTATIVE_SHORT_MSG) return MVX_ALG_RS_RECDBL;
+        return MVX_ALG_RS_PAIRWISE;
     case MVX_COLL_SCAN:          /* MPIR_intra_Scan, intra_scan.c:46-150 */
         return MVX_ALG_SCAN_RECDBL;
     default:
         return MVX_ALG_NONE;
     }
+}
+
+int mvx_plan_algorithm(int coll, int p, long total, int dtype)
+{
+    return mvx_plan_algorithm_kind(coll, p, total, dtype, MVX_OPKIND_PREDEFINED);
 }
 
 /* Does the op's result depend on which operand is inout?  For the IEEE
@@ -230,8 +241,12 @@ static int rs_halving_calls(int p, int rank, const int *recvcnts)
 }
 
 static int plan_body(mvx_plan *P, int coll, int p, int rank, long count,
-                     const int *recvcnts, int dtype, int op, int root)
+                     const int *recvcnts, int dtype, int op, int root, int kind)
 {
+    /* noncommutative user ops: every combine is uop(in = lower ranks,
+     * inout = higher ranks) (5610-5624, 4922-4936, 6660-6682,
+     * intra_scan.c:124-137), the same tree on every rank */
+    const int canon = kind == MVX_OPKIND_USER_NONCOMMUTE;
     int e, ts, lgn, pof2, rem, L, i, s, q;
     long cnts[MVX_MAXP], disps[MVX_MAXP];
 
@@ -241,7 +256,8 @@ static int plan_body(mvx_plan *P, int coll, int p, int rank, long count,
     for (i = 0; i < MVX_MAXK; i++) P->leaf_fold[i] = -1;
     P->coll = coll; P->p = p; P->rank = rank; P->root = root;
     P->op = op; P->dtype = dtype; P->esize = e;
-    P->symmetric = op_symmetric(op, dtype);
+    P->symmetric = kind == MVX_OPKIND_PREDEFINED && op_symmetric(op, dtype);
+    P->opkind = kind;
     P->shape = MVX_SHAPE_TREE;
 
     if (coll == MVX_COLL_REDUCE_SCATTER) {
@@ -251,7 +267,7 @@ static int plan_body(mvx_plan *P, int coll, int p, int rank, long count,
         count = total;
     }
     P->count = count;
-    P->alg = mvx_plan_algorithm(coll, p, count, dtype);
+    P->alg = mvx_plan_algorithm_kind(coll, p, count, dtype, kind);
     if (P->alg == MVX_ALG_NONE) return MPI_SUCCESS;   /* nothing to do */
 
     pof2 = pof2_lgn(p, &lgn);
@@ -261,7 +277,7 @@ static int plan_body(mvx_plan *P, int coll, int p, int rank, long count,
     if (coll == MVX_COLL_ALLREDUCE) {
         const int newrank = rank < 2 * rem ? (rank % 2 ? rank / 2 : -1) : rank - rem;
         P->calls_uop = (rank < 2 * rem && rank % 2) || (newrank != -1 && pof2 > 1);
-        if (P->alg == MVX_ALG_RECDBL && !P->symmetric) {
+        if (P->alg == MVX_ALG_RECDBL && !P->symmetric && !canon) {
             /* every rank needs every vector: its own-rooted tree differs */
             const int o = rank < 2 * rem ? rank / 2 : rank - rem;
             for (s = 0; s < p; s++) {
@@ -283,7 +299,10 @@ static int plan_body(mvx_plan *P, int coll, int p, int rank, long count,
             if (rank < pof2) set_range(&P->a_recv[s], disps[rank], cnts[rank]);
         }
         if (rank < pof2) {
-            const int o = P->symmetric ? 0 : bitrev(rank, L);
+            /* Rabenseifner: newrank o ends owning block bitrev(o); recursive
+             * doubling with a rank-independent tree (symmetric or
+             * noncommutative user op): any rank can combine any block */
+            const int o = (P->symmetric || canon) ? 0 : bitrev(rank, L);
             P->has_combine = 1;
             P->k = pof2;
             for (q = 0; q < pof2; q++) fold_leaf(o ^ q, rem, 1, &P->leaf[q], &P->leaf_fold[q]);
@@ -321,9 +340,12 @@ static int plan_body(mvx_plan *P, int coll, int p, int rank, long count,
                     if (s != root) set_range(&P->b_recv[s], disps[s], cnts[s]);
             return MPI_SUCCESS;
         }
-        /* binomial tree: gather every vector at root, combine there */
+        /* binomial tree: gather every vector at root, combine there.  A
+         * noncommutative op runs the tree relative to 0 and hands the result
+         * to root (4908-4909, 4956-4966): the same leaves from 0. */
+        const int lroot = canon ? 0 : root;
         {
-            const int rel = (rank - root + p) % p;
+            const int rel = (rank - lroot + p) % p;
             int m;
             for (m = 1; m < p; m <<= 1) {
                 if (rel & m) break;
@@ -338,7 +360,7 @@ static int plan_body(mvx_plan *P, int coll, int p, int rank, long count,
             if (s != root) set_range(&P->a_recv[s], 0, count);
         P->has_combine = 1;
         P->k = p;
-        for (q = 0; q < p; q++) P->leaf[q] = (q + root) % p;
+        for (q = 0; q < p; q++) P->leaf[q] = (q + lroot) % p;
         P->c_src_off = 0; P->c_cnt = count; P->c_dst_off = 0;
         return MPI_SUCCESS;
     }
@@ -365,10 +387,14 @@ static int plan_body(mvx_plan *P, int coll, int p, int rank, long count,
             const int dst = rank ^ (1 << l), size_l = 1 << l;
             int q, ll;
             if (!(rank & (1 << l))) continue;
-            for (q = 0; q < size_l; q++) P->leaf[pos + q] = dst ^ q;
+            /* noncommutative: dst's partial is the aligned block in rank
+             * order, lower ranks as `in` at every level */
+            for (q = 0; q < size_l; q++) P->leaf[pos + q] = canon ? ((dst >> l) << l) + q : dst ^ q;
             for (ll = 0; (1 << ll) < size_l; ll++)
-                for (q = 0; q + (1 << ll) < size_l; q += 2 << ll)
+                for (q = 0; q + (1 << ll) < size_l; q += 2 << ll) {
                     P->tree_mask |= 1u << (ll * 8 + pos + q);
+                    if (canon) P->tree_swap |= 1u << (ll * 8 + pos + q);
+                }
             P->chain_mask |= 1u << pos;
             pos += size_l;
         }
@@ -391,6 +417,14 @@ static int plan_body(mvx_plan *P, int coll, int p, int rank, long count,
             P->shape = MVX_SHAPE_CHAIN;
             P->k = p;
             for (q = 0; q < p; q++) P->leaf[q] = (rank - q + p) % p;
+            /* noncommutative: src = rank - q above rank swaps (6487-6498) */
+            for (q = 1; q < p; q++)
+                if (canon && q > rank) P->chain_swap |= 1u << q;
+        } else if (P->alg == MVX_ALG_RS_RECDBL) {
+            /* noncommutative recursive doubling (6505-6706): block r ends as
+             * the rank-ordered tree, lower ranks as `in` */
+            P->k = p;
+            for (q = 0; q < p; q++) P->leaf[q] = q;
         } else {
             const int o = rank < 2 * rem ? rank / 2 : rank - rem;
             P->calls_uop = rs_halving_calls(p, rank, recvcnts);
@@ -403,13 +437,24 @@ static int plan_body(mvx_plan *P, int coll, int p, int rank, long count,
     return MPI_ERR_ARG;
 }
 
-int mvx_plan_build(mvx_plan *P, int coll, int p, int rank, long count,
-                   const int *recvcnts, int dtype, int op, int root)
+int mvx_plan_build_kind(mvx_plan *P, int coll, int p, int rank, long count,
+                        const int *recvcnts, int dtype, int op, int root, int kind)
 {
-    int rc = plan_body(P, coll, p, rank, count, recvcnts, dtype, op, root);
+    int rc;
+    if (kind < MVX_OPKIND_PREDEFINED || kind > MVX_OPKIND_USER_NONCOMMUTE) return MPI_ERR_ARG;
+    rc = plan_body(P, coll, p, rank, count, recvcnts, dtype, op, root, kind);
     if (rc == MPI_SUCCESS && P->has_combine && P->shape >= 0) {
         P->tree_mask = P->shape == MVX_SHAPE_TREE ? tree_mask(P->k) : 0u;
         P->chain_mask = P->shape == MVX_SHAPE_CHAIN ? chain_mask(P->k) : 0u;
+        if (kind == MVX_OPKIND_USER_NONCOMMUTE && P->shape == MVX_SHAPE_TREE)
+            P->tree_swap = P->tree_mask;
     }
     return rc;
+}
+
+int mvx_plan_build(mvx_plan *P, int coll, int p, int rank, long count,
+                   const int *recvcnts, int dtype, int op, int root)
+{
+    return mvx_plan_build_kind(P, coll, p, rank, count, recvcnts, dtype, op, root,
+                               MVX_OPKIND_PREDEFINED);
 }

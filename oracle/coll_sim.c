@@ -20,8 +20,11 @@
  *     binomial tree 4876-4954.
  *   orc_reduce_scatter  intra_fns_new.c:6191-6503
  *     recursive halving 6248-6448 (fold 6283-6312, counts 6325-6339,
- *     mask pof2/2 -> 1 6341-6407), pairwise 6450-6503.
- * Only predefined (commutative, permanent) ops are simulated.
+ *     mask pof2/2 -> 1 6341-6407), pairwise 6450-6503 (noncommutative
+ *     operand swap 6487-6498), noncommutative recursive doubling 6505-6706.
+ * User ops (orc_user_op_set) take the permanent == 0 choices (recursive
+ * doubling 5590, binomial 4620) and every `commute` branch: 5610-5624,
+ * 4908-4936 / 4956-4966, 6487, 6660-6682, intra_scan.c:124-137.
  */
 #include <stdlib.h>
 #include <string.h>
@@ -39,7 +42,8 @@ static const int coll_table_flat[3 * 5] = {
     -1, 65536, 4096, 4096, 4096 };
 #define ALLREDUCE_IDX 1
 #define REDUCE_IDX 2
-#define REDSCAT_COMMUTATIVE_LONG_MSG 524288
+#define REDSCAT_COMMUTATIVE_LONG_MSG 524288   /* intra_fns_new.c:39-40 */
+#define REDSCAT_NONCOMMUTATIVE_SHORT_MSG 512
 
 static int pof2_lgn(int size, int *lgn_out)
 {
@@ -58,7 +62,23 @@ static int imul32(long a, long b)
     return (int)(unsigned int)((unsigned long)a * (unsigned long)b);
 }
 
-static int op_valid(int op) { return op >= 100 && op <= 111; }
+#define NUOPS 64
+static struct { orc_user_fn *fn; int commute; } g_uops[NUOPS];
+
+int orc_user_op_set(int handle, orc_user_fn *fn, int commute)
+{
+    if (handle < 200 || handle >= 200 + NUOPS) return 12;
+    g_uops[handle - 200].fn = fn;
+    g_uops[handle - 200].commute = commute;
+    return 0;
+}
+
+static int permanent(int op) { return op >= 100 && op <= 111; }
+static int op_valid(int op)
+{
+    return permanent(op) || (op >= 200 && op < 200 + NUOPS && g_uops[op - 200].fn);
+}
+static int commute(int op) { return permanent(op) ? 1 : g_uops[op - 200].commute; }
 
 /* copy n elements, only the bytes in the datatype's type map (MPI message
  * semantics: padding of the destination is left alone) */
@@ -89,36 +109,71 @@ static char *dup_buf(const void *src, long bytes)
 static void uop(int op, int dtype, const void *in, void *inout, int len,
                 int *err)
 {
-    int e = orc_op(op, dtype, in, inout, len);
+    int e;
+    if (!permanent(op)) {     /* user functions report nothing */
+        int l = len, t = dtype;
+        g_uops[op - 200].fn((void *)in, inout, &l, &t);
+        return;
+    }
+    e = orc_op(op, dtype, in, inout, len);
     if (e) *err = e;
 }
 
-int orc_algorithm(int coll, int p, long total_count, int dtype)
+int orc_call(int op, int dtype, const void *in, void *inout, int len)
+{
+    int err = 0;
+    if (!op_valid(op)) return ERR_OP;
+    uop(op, dtype, in, inout, len, &err);
+    return err;
+}
+
+/* the noncommutative "order is not right" step: uop(mine, theirs) into a
+ * copy of theirs, copied back into mine (5615-5624 and its siblings) */
+static void uop_swapped(int op, int dtype, const void *theirs, void *mine, int len,
+                        int *err)
+{
+    int E, TS;
+    char *tmp;
+    orc_dtype_info(dtype, &E, &TS);
+    tmp = dup_buf(theirs, (long)len * E);
+    uop(op, dtype, mine, tmp, len, err);
+    tm_copy(mine, tmp, len, dtype);
+    free(tmp);
+}
+
+int orc_algorithm_op(int coll, int p, long total_count, int dtype, int op)
 {
     int e, ts, lgn, pof2, tv;
+    const int perm = permanent(op), comm = op_valid(op) ? commute(op) : 1;
     if (orc_dtype_info(dtype, &e, &ts)) return ORC_ALG_NONE;
     pof2 = pof2_lgn(p, &lgn);
     if (coll == ORC_COLL_ALLREDUCE) {
         if (total_count == 0) return ORC_ALG_NONE;
         tv = coll_table_flat[ALLREDUCE_IDX * 5 + lgn];
-        if (tv == -1 || imul32(total_count, ts) < tv || total_count < pof2)
+        if (tv == -1 || imul32(total_count, ts) < tv || !perm || total_count < pof2)
             return ORC_ALG_RECDBL;
         return ORC_ALG_RABENSEIFNER;
     }
     if (coll == ORC_COLL_REDUCE) {
         if (total_count == 0) return ORC_ALG_NONE;
         tv = coll_table_flat[REDUCE_IDX * 5 + lgn];
-        if (tv != -1 && imul32(total_count, ts) > tv && total_count >= pof2)
+        if (tv != -1 && imul32(total_count, ts) > tv && perm && total_count >= pof2)
             return ORC_ALG_RABENSEIFNER;
         return ORC_ALG_BINOMIAL;
     }
     if (coll == ORC_COLL_REDUCE_SCATTER) {
+        const int nbytes = imul32(total_count, ts);
         if (total_count == 0) return ORC_ALG_NONE;
-        if (imul32(total_count, ts) < REDSCAT_COMMUTATIVE_LONG_MSG)
-            return ORC_ALG_RS_HALVING;
+        if (comm && nbytes < REDSCAT_COMMUTATIVE_LONG_MSG) return ORC_ALG_RS_HALVING;
+        if (!comm && nbytes < REDSCAT_NONCOMMUTATIVE_SHORT_MSG) return ORC_ALG_RS_RECDBL;
         return ORC_ALG_RS_PAIRWISE;
     }
     return ORC_ALG_NONE;
+}
+
+int orc_algorithm(int coll, int p, long total_count, int dtype)
+{
+    return orc_algorithm_op(coll, p, total_count, dtype, 102);
 }
 
 /* ---------------------------------------------------------------------- */
@@ -163,7 +218,7 @@ int orc_allreduce(int p, const void *const *send, void *const *recv,
         } else newrank[r] = r - rem;
     }
 
-    alg = orc_algorithm(ORC_COLL_ALLREDUCE, p, count, dtype);
+    alg = orc_algorithm_op(ORC_COLL_ALLREDUCE, p, count, dtype, op);
 #define REAL(nd) (((nd) < rem) ? (nd) * 2 + 1 : (nd) + rem)
     if (alg == ORC_ALG_RECDBL) {
         for (mask = 1; mask < pof2; mask <<= 1) {
@@ -173,7 +228,8 @@ int orc_allreduce(int p, const void *const *send, void *const *recv,
                 int dst;
                 if (newrank[r] == -1) continue;
                 dst = REAL(newrank[r] ^ mask);
-                uop(op, dtype, snap[dst], recv[r], count, &err[r]);
+                if (commute(op) || dst < r) uop(op, dtype, snap[dst], recv[r], count, &err[r]);
+                else uop_swapped(op, dtype, snap[dst], recv[r], count, &err[r]);
             }
             for (r = 0; r < p; r++) { free(snap[r]); snap[r] = NULL; }
         }
@@ -296,7 +352,7 @@ int orc_reduce(int p, const void *const *send, void *const *recv,
         tm_copy(wb[r], send[r], count, dtype);
     }
     pof2 = pof2_lgn(p, &lgn);
-    alg = orc_algorithm(ORC_COLL_REDUCE, p, count, dtype);
+    alg = orc_algorithm_op(ORC_COLL_REDUCE, p, count, dtype, op);
 
     if (alg == ORC_ALG_RABENSEIFNER) {
         int *newrank = (int *)calloc((size_t)p, sizeof(int));
@@ -426,28 +482,33 @@ int orc_reduce(int p, const void *const *send, void *const *recv,
         free(newrank); free(cnts); free(disps); free(sidx); free(ridx);
         free(lidx); free(rcnt); free(active); free(jj);
     } else {
-        /* binomial tree relative to root (commutative: lroot = root) */
+        /* binomial tree relative to lroot: root if commutative, else 0
+         * and the result is sent on to root (4908-4909, 4956-4966) */
+        const int lroot = commute(op) ? root : 0;
         for (mask = 1; mask < p; mask <<= 1) {
             int *recv_from = (int *)malloc(sizeof(int) * (size_t)p);
             for (r = 0; r < p; r++) {
-                int rel = (r - root + p) % p, src;
+                int rel = (r - lroot + p) % p, src;
                 recv_from[r] = -1;
                 /* a rank that already sent has exited: its low bits hold a 1 */
                 if (rel & (mask - 1)) continue;
                 if ((mask & rel) == 0) {
                     src = rel | mask;
-                    if (src < p) recv_from[r] = (src + root) % p;
+                    if (src < p) recv_from[r] = (src + lroot) % p;
                 }
             }
             for (r = 0; r < p; r++)
                 if (recv_from[r] >= 0)
                     snap[recv_from[r]] = dup_buf(wb[recv_from[r]], bytes);
-            for (r = 0; r < p; r++)
-                if (recv_from[r] >= 0)
-                    uop(op, dtype, snap[recv_from[r]], wb[r], count, &err[r]);
+            for (r = 0; r < p; r++) {
+                if (recv_from[r] < 0) continue;
+                if (commute(op)) uop(op, dtype, snap[recv_from[r]], wb[r], count, &err[r]);
+                else uop_swapped(op, dtype, snap[recv_from[r]], wb[r], count, &err[r]);
+            }
             for (r = 0; r < p; r++) { free(snap[r]); snap[r] = NULL; }
             free(recv_from);
         }
+        if (lroot != root) tm_copy(wb[root], wb[0], count, dtype);
     }
     for (r = 0; r < p; r++) {
         rc[r] = err[r];
@@ -458,6 +519,110 @@ int orc_reduce(int p, const void *const *send, void *const *recv,
 }
 
 /* ---------------------------------------------------------------------- */
+
+/* Noncommutative short-message Reduce_scatter, intra_fns_new.c:6505-6706:
+ * recursive doubling over the whole vector; each step moves every block but
+ * the sender's subtree's (an indexed type of two runs), the subtrees that
+ * lack a partner in the non-power-of-two case get the received data
+ * forwarded down a halving tree (6598-6650), and the combine is done after
+ * the forwarding (6652-6682).  Lockstep: every message of a round is read
+ * from the sender's state at the start of that round. */
+typedef struct { int len0, len1, dis1; } twoblk;
+
+static twoblk except_subtree(const int *recvcnts, int p, int root, int mask)
+{
+    twoblk t;
+    int j;
+    t.len0 = t.len1 = 0;
+    for (j = 0; j < root && j < p; j++) t.len0 += recvcnts[j];
+    for (j = root + mask; j < p; j++) t.len1 += recvcnts[j];
+    t.dis1 = t.len0;
+    for (j = root; j < root + mask && j < p; j++) t.dis1 += recvcnts[j];
+    return t;
+}
+
+static void copy_two(char *dst, const char *src, twoblk t, int E, int dtype)
+{
+    tm_copy(dst, src, t.len0, dtype);
+    tm_copy(dst + (long)t.dis1 * E, src + (long)t.dis1 * E, t.len1, dtype);
+}
+
+static void rs_recdbl(int p, const void *const *send, void *const *recv,
+                      const int *recvcnts, const int *disps, int total, int dtype,
+                      int op, int *err)
+{
+    int E, TS, r, mask, i;
+    long bytes;
+    char **res, **tmp, **snap;
+    int *received, *dtr, *mtr;
+    orc_dtype_info(dtype, &E, &TS);
+    bytes = (long)total * E;
+    res = (char **)calloc((size_t)p, sizeof(char *));
+    tmp = (char **)calloc((size_t)p, sizeof(char *));
+    snap = (char **)calloc((size_t)p, sizeof(char *));
+    received = (int *)calloc((size_t)p, sizeof(int));
+    dtr = (int *)calloc((size_t)p, sizeof(int));
+    mtr = (int *)calloc((size_t)p, sizeof(int));
+    for (r = 0; r < p; r++) {
+        res[r] = (char *)calloc((size_t)bytes + 1, 1);
+        tmp[r] = (char *)calloc((size_t)bytes + 1, 1);
+        tm_copy(res[r], send[r], total, dtype);
+    }
+    for (mask = 1, i = 0; mask < p; mask <<= 1, i++) {
+        int tmask, k, kk;
+        for (r = 0; r < p; r++) {
+            dtr[r] = ((r ^ mask) >> i) << i;
+            mtr[r] = (r >> i) << i;
+            received[r] = 0;
+        }
+        /* the exchange: rank r receives dst's tmp_results minus r's
+         * partner subtree (dst's sendtype = r's recvtype) */
+        for (r = 0; r < p; r++) snap[r] = dup_buf(res[r], bytes);
+        for (r = 0; r < p; r++) {
+            const int dst = r ^ mask;
+            if (dst >= p) continue;
+            copy_two(tmp[r], snap[dst], except_subtree(recvcnts, p, dtr[r], mask), E, dtype);
+            received[r] = 1;
+        }
+        for (r = 0; r < p; r++) { free(snap[r]); snap[r] = NULL; }
+        /* forwarding inside subtrees that had no partner */
+        for (kk = mask, k = 0; kk; kk >>= 1) k++;
+        k--;
+        for (tmask = mask >> 1; tmask; tmask >>= 1, k--) {
+            for (r = 0; r < p; r++) snap[r] = dup_buf(tmp[r], bytes);
+            for (r = 0; r < p; r++) {
+                int dst = r ^ tmask, tree_root, done;
+                if (dtr[r] + mask <= p) continue;
+                done = p - mtr[r] - mask;
+                tree_root = (r >> k) << k;
+                if (dst < r && dst < tree_root + done && r >= tree_root + done) {
+                    copy_two(tmp[r], snap[dst], except_subtree(recvcnts, p, dtr[r], mask), E, dtype);
+                    received[r] = 1;
+                }
+            }
+            for (r = 0; r < p; r++) { free(snap[r]); snap[r] = NULL; }
+        }
+        /* the combine, over the two runs of the recvtype */
+        for (r = 0; r < p; r++) {
+            twoblk t;
+            if (!received[r]) continue;
+            t = except_subtree(recvcnts, p, dtr[r], mask);
+            if (commute(op) || dtr[r] < mtr[r]) {
+                uop(op, dtype, tmp[r], res[r], t.len0, &err[r]);
+                uop(op, dtype, tmp[r] + (long)t.dis1 * E, res[r] + (long)t.dis1 * E, t.len1, &err[r]);
+            } else {
+                uop(op, dtype, res[r], tmp[r], t.len0, &err[r]);
+                uop(op, dtype, res[r] + (long)t.dis1 * E, tmp[r] + (long)t.dis1 * E, t.len1, &err[r]);
+                copy_two(res[r], tmp[r], t, E, dtype);
+            }
+        }
+    }
+    for (r = 0; r < p; r++) {
+        if (recvcnts[r]) tm_copy(recv[r], res[r] + (long)disps[r] * E, recvcnts[r], dtype);
+        free(res[r]); free(tmp[r]);
+    }
+    free(res); free(tmp); free(snap); free(received); free(dtr); free(mtr);
+}
 
 int orc_reduce_scatter(int p, const void *const *send, void *const *recv,
                        const int *recvcnts, int dtype, int op, int *rc)
@@ -477,7 +642,7 @@ int orc_reduce_scatter(int p, const void *const *send, void *const *recv,
     for (i = 0; i < p; i++) { disps[i] = total; total += recvcnts[i]; }
     if (total == 0) { free(disps); free(err); return 0; }
 
-    alg = orc_algorithm(ORC_COLL_REDUCE_SCATTER, p, total, dtype);
+    alg = orc_algorithm_op(ORC_COLL_REDUCE_SCATTER, p, total, dtype, op);
     if (alg == ORC_ALG_RS_HALVING) {
         int lgn, pof2 = pof2_lgn(p, &lgn), rem = p - pof2, mask;
         long bytes = (long)total * E;
@@ -555,7 +720,7 @@ int orc_reduce_scatter(int p, const void *const *send, void *const *recv,
         for (r = 0; r < p; r++) free(res[r]);
         free(res); free(snap); free(newrank); free(newcnts); free(newdisps);
         free(sidx); free(ridx); free(lidx); free(rcnt);
-    } else {
+    } else if (alg == ORC_ALG_RS_PAIRWISE) {
         /* pairwise: rank r folds in block r of rank r-1, r-2, ... */
         for (r = 0; r < p; r++)
             tm_copy(recv[r], (const char *)send[r] + (long)disps[r] * E,
@@ -566,10 +731,13 @@ int orc_reduce_scatter(int p, const void *const *send, void *const *recv,
                 long n = recvcnts[r];
                 char *tmp = (char *)calloc((size_t)(n * E + 1), 1);
                 tm_copy(tmp, (const char *)send[src] + (long)disps[r] * E, n, dtype);
-                uop(op, dtype, tmp, recv[r], recvcnts[r], &err[r]);
+                if (commute(op) || src < r) uop(op, dtype, tmp, recv[r], recvcnts[r], &err[r]);
+                else uop_swapped(op, dtype, tmp, recv[r], recvcnts[r], &err[r]);
                 free(tmp);
             }
         }
+    } else {
+        rs_recdbl(p, send, recv, recvcnts, disps, total, dtype, op, err);
     }
     for (r = 0; r < p; r++) rc[r] = err[r];
     free(disps); free(err);
@@ -608,8 +776,10 @@ int orc_scan(int p, const void *const *send, void *const *recv, int count,
             if (r > dst) {
                 uop(op, dtype, snap[dst], partial[r], count, &dummy);
                 uop(op, dtype, snap[dst], recv[r], count, &dummy);
-            } else {
+            } else if (commute(op)) {
                 uop(op, dtype, snap[dst], partial[r], count, &dummy);
+            } else {
+                uop_swapped(op, dtype, snap[dst], partial[r], count, &dummy);
             }
         }
         for (r = 0; r < p; r++) { free(snap[r]); snap[r] = NULL; }

@@ -10,8 +10,8 @@
  *                         reference src/coll/global_ops.c:56-1745
  *   orc_allreduce()       intra_Allreduce, src/coll/intra_fns_new.c:5453-5790
  *   orc_reduce()          intra_Reduce,    src/coll/intra_fns_new.c:4519-4989
- *   orc_reduce_scatter()  intra_Reduce_scatter (commutative branches),
- *                         src/coll/intra_fns_new.c:6191-6503
+ *   orc_reduce_scatter()  intra_Reduce_scatter, src/coll/intra_fns_new.c:
+ *                         6191-6720 (all four branches)
  *   orc_scan()            MPIR_intra_Scan, src/coll/intra_scan.c:91-150
  * The collectives are simulated with p in-memory ranks stepping in lockstep
  * through the reference's own send/recv schedule (every round snapshots the
@@ -52,6 +52,14 @@ int orc_reduce(int p, const void *const *send, void *const *recv,
 int orc_reduce_scatter(int p, const void *const *send, void *const *recv,
                        const int *recvcnts, int dtype, int op, int *rc);
 
+/* User-defined ops (MPI_Op_create, opcreate.c:62-76): handles 200..263
+ * name an MPI_User_function with its commute flag; the replays then take the
+ * reference's permanent == 0 and noncommutative branches.  fn = NULL frees. */
+typedef void orc_user_fn(void *invec, void *inoutvec, int *len, int *dtype);
+int orc_user_op_set(int handle, orc_user_fn *fn, int commute);
+/* orc_op for any handle, user ops included */
+int orc_call(int op, int dtype, const void *in, void *inout, int len);
+
 /* MPI_Scan, the default MPIR_intra_Scan (intra_scan.c:91-150) */
 int orc_scan(int p, const void *const *send, void *const *recv, int count,
              int dtype, int op, int *rc);
@@ -64,7 +72,10 @@ int orc_scan(int p, const void *const *send, void *const *recv, int count,
 #define ORC_ALG_BINOMIAL      3  /* Reduce binomial tree                  */
 #define ORC_ALG_RS_HALVING    4  /* Reduce_scatter recursive halving      */
 #define ORC_ALG_RS_PAIRWISE   5  /* Reduce_scatter pairwise exchange      */
+#define ORC_ALG_RS_RECDBL     7  /* Reduce_scatter recursive doubling
+                                    (noncommutative, < 512 bytes)         */
 int orc_algorithm(int coll, int p, long total_count, int dtype);
+int orc_algorithm_op(int coll, int p, long total_count, int dtype, int op);
 #define ORC_COLL_ALLREDUCE      1
 #define ORC_COLL_REDUCE         2
 #define ORC_COLL_REDUCE_SCATTER 3

@@ -16,6 +16,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "liboracle.so")
 
 ALG_NONE, ALG_RECDBL, ALG_RABENSEIFNER, ALG_BINOMIAL, ALG_RS_HALVING, ALG_RS_PAIRWISE = range(6)
+ALG_RS_RECDBL = 7
 COLL_ALLREDUCE, COLL_REDUCE, COLL_REDUCE_SCATTER = 1, 2, 3
 
 _lib = None
@@ -34,6 +35,7 @@ def lib():
         vp = ctypes.c_void_p
         L.orc_dtype_info.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
         L.orc_op.argtypes = [ctypes.c_int, ctypes.c_int, vp, vp, ctypes.c_int]
+        L.orc_call.argtypes = [ctypes.c_int, ctypes.c_int, vp, vp, ctypes.c_int]
         L.orc_allreduce.argtypes = [ctypes.c_int, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.c_int,
                                     ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
         L.orc_reduce.argtypes = [ctypes.c_int, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.c_int,
@@ -44,6 +46,8 @@ def lib():
         L.orc_scan.argtypes = [ctypes.c_int, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.c_int,
                                ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
         L.orc_algorithm.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_long, ctypes.c_int]
+        L.orc_algorithm_op.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_long, ctypes.c_int, ctypes.c_int]
+        L.orc_user_op_set.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
         L.orc_fill.argtypes = [vp, ctypes.c_long, ctypes.c_int, ctypes.c_int]
         L.orc_fill.restype = None
         _lib = L
@@ -63,8 +67,9 @@ def dtype_info(dtype):
 
 
 def op(op_handle, dtype, invec, inoutvec, count):
-    """inoutvec = invec op inoutvec (in place, numpy uint8 views). Returns rc."""
-    return lib().orc_op(op_handle, dtype, _ptr(invec), _ptr(inoutvec), count)
+    """inoutvec = invec op inoutvec (in place, numpy uint8 views). Returns rc.
+    User op handles (user_op_set) call the registered function."""
+    return lib().orc_call(op_handle, dtype, _ptr(invec), _ptr(inoutvec), count)
 
 
 def _ptrs(bufs):
@@ -103,8 +108,15 @@ def scan(sends, recvs, count, dtype, op_handle):
     return list(rc)
 
 
-def algorithm(coll, p, total_count, dtype):
-    return lib().orc_algorithm(coll, p, total_count, dtype)
+def algorithm(coll, p, total_count, dtype, op=None):
+    if op is None:
+        return lib().orc_algorithm(coll, p, total_count, dtype)
+    return lib().orc_algorithm_op(coll, p, total_count, dtype, op)
+
+
+def user_op_set(handle, fn_addr, commute):
+    """Register an MPI_User_function (C address) as user op `handle` (200..263)."""
+    return lib().orc_user_op_set(handle, fn_addr, commute)
 
 
 def fill(nbytes_or_array, n, dist, rank):

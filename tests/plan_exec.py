@@ -28,8 +28,9 @@ def chain_mask(k):
     return ((1 << k) - 1) & ~1 if k >= 2 else 0
 
 
-def run_program(op, dtype, leaves, folds, tmask, cmask, n):
-    """The combine program of include/mvx_hip.h, step by step with the oracle op."""
+def run_program(op, dtype, leaves, folds, tmask, cmask, n, tswap=0, cswap=0):
+    """The combine program of include/mvx_hip.h, step by step with the oracle
+    op; a swapped step (user ops) is y_left = uop(in = y_left, inout = y_right)."""
     y = []
     for q, a in enumerate(leaves):
         v = a.copy()
@@ -41,10 +42,20 @@ def run_program(op, dtype, leaves, folds, tmask, cmask, n):
         for q in range(8):
             if tmask >> (l * 8 + q) & 1:
                 assert q + (1 << l) < k
-                O.op(op, dtype, y[q + (1 << l)], y[q], n)
+                if tswap >> (l * 8 + q) & 1:
+                    O.op(op, dtype, y[q], y[q + (1 << l)], n)
+                    y[q] = y[q + (1 << l)]
+                else:
+                    O.op(op, dtype, y[q + (1 << l)], y[q], n)
+            else:
+                assert not tswap >> (l * 8 + q) & 1
     for q in range(1, k):
         if cmask >> q & 1:
-            O.op(op, dtype, y[q], y[0], n)
+            if cswap >> q & 1:
+                O.op(op, dtype, y[0], y[q], n)
+                y[0] = y[q]
+            else:
+                O.op(op, dtype, y[q], y[0], n)
     return y[0]
 
 
@@ -72,7 +83,8 @@ def run_plans(plans, sends, recvs):
                     assert plans[s].a_send[r].cnt == P.a_recv[s].cnt and plans[s].a_send[r].off == P.a_recv[s].off
         leaves = [sends[P.leaf[q]][lo:hi] for q in range(P.k)]
         folds = [sends[P.leaf_fold[q]][lo:hi] if P.leaf_fold[q] >= 0 else None for q in range(P.k)]
-        out = run_program(P.op, P.dtype, leaves, folds, P.tree_mask, P.chain_mask, P.c_cnt)
+        out = run_program(P.op, P.dtype, leaves, folds, P.tree_mask, P.chain_mask, P.c_cnt,
+                          P.tree_swap, P.chain_swap)
         outs[r] = out
         if not P.c_dst_tmp:
             d = P.c_dst_off * E

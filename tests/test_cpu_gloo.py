@@ -32,6 +32,9 @@ CASES = [  # (coll, count, dtype, op, root)
     (2, 10, 6, 102, 0), (2, 30000, 10, 102, 1), (2, 30000, 11, 101, 0), (2, 5000, 17, 110, 1),
     (3, 7, 6, 102, 0), (3, 200, 10, 102, 0), (3, 60000, 10, 102, 0), (3, 60000, 8, 105, 0),
     (3, 5000, 17, 111, 0), (4, 10, 6, 102, 0), (4, 3000, 10, 102, 0), (4, 700, 17, 110, 0),
+    # user ops (tests/user_ops.c): "name:commute"
+    (1, 3000, 7, "mix:0", 0), (1, 3000, 7, "mix:1", 0), (2, 2000, 9, "affine:0", 1),
+    (3, 20, 7, "mix:0", 0), (3, 300, 7, "mix:0", 0), (4, 500, 9, "affine:0", 0), (3, 300, 10, "fsum:1", 0),
 ]
 
 
@@ -43,6 +46,7 @@ def _worker(rank, world, port, out_dir):
     import torch.distributed as dist
 
     import mvxtest as T
+    import uops
     from oracle import oracle as O
     from plan_exec import run_program
 
@@ -52,7 +56,14 @@ def _worker(rank, world, port, out_dir):
     for ci, (coll, n, dtype, op, root) in enumerate(CASES):
         cnts = [n + (r % 3) for r in range(world)] if coll == 3 else None
         tot = sum(cnts) if cnts else n
-        S = [T.rand_vec(dtype, tot, 1000 * ci + r) for r in range(world)]
+        kind = None
+        if isinstance(op, str):
+            name, commute = op.split(":")
+            op, kind = 250, (1 if commute == "1" else 2)
+            O.user_op_set(op, uops.host_fn(name), int(commute))
+            S = [uops.rand_for(name, tot, 1000 * ci + r) for r in range(world)]
+        else:
+            S = [T.rand_vec(dtype, tot, 1000 * ci + r) for r in range(world)]
         E = S[0].dtype.itemsize
         sb = [s.view(np.uint8) for s in S]
         # oracle: the reference schedule over all ranks
@@ -76,7 +87,7 @@ def _worker(rank, world, port, out_dir):
             O.reduce_scatter(sb, [x.view(np.uint8) for x in R0], cnts, dtype, op)
             mine = R0[rank][: cnts[rank]]
             recvbuf = np.zeros(max(cnts[rank], 1) * E, np.uint8)
-        P = mvx.plan(coll, world, rank, n, dtype, op, root, cnts)
+        P = mvx.plan(coll, world, rank, n, dtype, op, root, cnts, opkind=kind)
         send = sb[rank]
         # phase A
         reqs, slot = [], {}
@@ -98,7 +109,8 @@ def _worker(rank, world, port, out_dir):
                 return send[lo:hi] if s == rank else slot[s].numpy()
             leaves = [leaf(P.leaf[q]) for q in range(P.k)]
             folds = [leaf(P.leaf_fold[q]) if P.leaf_fold[q] >= 0 else None for q in range(P.k)]
-            out = run_program(op, dtype, leaves, folds, P.tree_mask, P.chain_mask, P.c_cnt)
+            out = run_program(op, dtype, leaves, folds, P.tree_mask, P.chain_mask, P.c_cnt,
+                              P.tree_swap, P.chain_swap)
             if not P.c_dst_tmp:
                 recvbuf[P.c_dst_off * E: P.c_dst_off * E + out.size] = out
         # phase C
@@ -117,7 +129,10 @@ def _worker(rank, world, port, out_dir):
                 q.wait()
         if mine is not None:
             try:
-                T.assert_same(op, dtype, recvbuf[: mine.nbytes], mine, typemap_only=True)
+                if kind is not None:
+                    assert np.array_equal(recvbuf[: mine.nbytes], mine.view(np.uint8)), "user op result differs"
+                else:
+                    T.assert_same(op, dtype, recvbuf[: mine.nbytes], mine, typemap_only=True)
             except AssertionError as e:
                 failures.append("case %d rank %d: %s" % (ci, rank, e))
         dist.barrier()
