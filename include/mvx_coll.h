@@ -170,6 +170,44 @@ int mvx_op_errno(void);
 #define MVX_ALG_RS_PAIRWISE   5
 #define MVX_ALG_SCAN_RECDBL   6
 #define MVX_ALG_RS_RECDBL     7   /* noncommutative Reduce_scatter < 512 bytes */
+#define MVX_ALG_SMP_LEADER    8   /* _SMP_ builds: node leader's sequential fold
+                                     (intra_shmem_Reduce / intra_shmem_Allreduce) */
+
+/* ---- device flavour and collective knobs -------------------------------
+ * The reference picks its collops at build time: the ch_shmem device (no
+ * _SMP_, the flavour SURVEY.md's oracle was built as) installs intra_Reduce /
+ * intra_Allreduce; the _SMP_ devices (ch_gen2, ch_smp, ch_gen2_ud) install
+ * intra_shmem_Reduce / intra_shmem_Allreduce in front of them
+ * (intra_fns_new.c:293-310), whose small-message path is a leader folding the
+ * node's ranks in rank order (4992-5198, 5793-5940), with runtime knobs read
+ * by MPIR_Init (initutil.c:230-293).  Here the flavour is per communicator. */
+typedef struct mvx_tuning {
+    int smp;                        /* 1: _SMP_ collops, 0: ch_shmem collops  */
+    int enable_shmem_collectives;   /* initutil.c:146; VIADEV_USE_SHMEM_COLL=0,
+                                       VIADEV_USE_BLOCKING=1, (MV|VIADEV)_USE_
+                                       SHARED_MEM=0 clear it                  */
+    int shmem_coll_ok;              /* the comm holds a shmem collective block
+                                       (create_2level_comm.c:199-225, 274-279) */
+    int disable_shmem_reduce;       /* !VIADEV_USE_SHMEM_REDUCE              */
+    int disable_shmem_allreduce;    /* !VIADEV_USE_SHMEM_ALLREDUCE           */
+    int shmem_coll_reduce_threshold;     /* bytes, default 1 << 10 (:70)    */
+    int shmem_coll_allreduce_threshold;  /* bytes, default 1 << 15 (:71)    */
+} mvx_tuning;
+
+/* The knobs of an `smp` build after MPIR_Init's environment parsing
+ * (VIADEV_USE_SHMEM_REDUCE, VIADEV_USE_SHMEM_ALLREDUCE, VIADEV_USE_BLOCKING,
+ * VIADEV_USE_SHMEM_COLL, VIADEV_USE_SHARED_MEM, MV_USE_SHARED_MEM,
+ * VIADEV_SHMEM_COLL_MAX_MSG_SIZE, VIADEV_SHMEM_COLL_{REDUCE,ALLREDUCE}_
+ * THRESHOLD); shmem_coll_ok = 1.  Returns MPI_ERR_OTHER where the reference
+ * prints and exits (a threshold above the max message size, :289-293). */
+int mvx_tuning_from_env(mvx_tuning *t, int smp);
+/* Communicators take their flavour from MVX_DEVICE at creation: "ch_gen2",
+ * "ch_smp" or "ch_gen2_ud" select the _SMP_ collops, anything else (default
+ * "ch_shmem") the plain ones.  An _SMP_ communicator claims one of the
+ * VIADEV_MAX_SHMEM_COLL_COMM (default 16) shmem blocks, as create_2level_comm
+ * does; without one its shmem_coll_ok is 0. */
+int mvx_comm_get_tuning(MPI_Comm comm, mvx_tuning *t);
+int mvx_comm_set_tuning(MPI_Comm comm, const mvx_tuning *t);
 
 /* What kind of op a plan is for: the reference's struct MPIR_OP
  * {permanent, commute} (include/mpiops.h:1-11) */
@@ -217,9 +255,15 @@ int mvx_plan_build(mvx_plan *plan, int coll, int p, int rank, long count,
  * noncommutative op takes the reference's order-preserving branches. */
 int mvx_plan_build_kind(mvx_plan *plan, int coll, int p, int rank, long count,
                         const int *recvcnts, int dtype, int op, int root, int opkind);
+/* The same under a device flavour (NULL = ch_shmem). */
+int mvx_plan_build_tuned(mvx_plan *plan, int coll, int p, int rank, long count,
+                         const int *recvcnts, int dtype, int op, int root, int opkind,
+                         const mvx_tuning *t);
 /* The reference's algorithm for (coll, p, total elements, dtype[, opkind]). */
 int mvx_plan_algorithm(int coll, int p, long total_count, int dtype);
 int mvx_plan_algorithm_kind(int coll, int p, long total_count, int dtype, int opkind);
+int mvx_plan_algorithm_tuned(int coll, int p, long total_count, int dtype, int opkind,
+                             const mvx_tuning *t);
 /* Datatype facts: extent and MPI_Type_size; returns 0 or MPI_ERR_TYPE. */
 int mvx_dtype_info(int dtype, int *extent, int *type_size);
 

@@ -67,6 +67,15 @@ class Plan(ctypes.Structure):
     ]
 
 
+class Tuning(ctypes.Structure):
+    """Mirror of ``mvx_tuning`` (include/mvx_coll.h): device flavour + knobs."""
+    _fields_ = [
+        ("smp", ctypes.c_int), ("enable_shmem_collectives", ctypes.c_int), ("shmem_coll_ok", ctypes.c_int),
+        ("disable_shmem_reduce", ctypes.c_int), ("disable_shmem_allreduce", ctypes.c_int),
+        ("shmem_coll_reduce_threshold", ctypes.c_int), ("shmem_coll_allreduce_threshold", ctypes.c_int),
+    ]
+
+
 def _load():
     global _hip, _coll
     if _coll is not None:
@@ -132,6 +141,12 @@ def _load():
     c.mvx_plan_build_kind.argtypes = [ctypes.POINTER(Plan), i, i, i, ctypes.c_long, pi, i, i, i, i]
     c.mvx_plan_algorithm_kind.argtypes = [i, i, ctypes.c_long, i, i]
     c.mvx_dtype_info.argtypes = [i, pi, pi]
+    pt = ctypes.POINTER(Tuning)
+    c.mvx_plan_build_tuned.argtypes = [ctypes.POINTER(Plan), i, i, i, ctypes.c_long, pi, i, i, i, i, pt]
+    c.mvx_plan_algorithm_tuned.argtypes = [i, i, ctypes.c_long, i, i, pt]
+    c.mvx_tuning_from_env.argtypes = [pt, i]
+    c.mvx_comm_get_tuning.argtypes = [i, pt]
+    c.mvx_comm_set_tuning.argtypes = [i, pt]
     for name in ("MPIR_MAXF", "MPIR_MINF", "MPIR_SUM", "MPIR_PROD", "MPIR_LAND", "MPIR_BAND", "MPIR_LOR",
                  "MPIR_BOR", "MPIR_LXOR", "MPIR_BXOR", "MPIR_MAXLOC", "MPIR_MINLOC"):
         fn = getattr(c, name)
@@ -157,13 +172,17 @@ def loaded_paths():
 
 # ---------------------------------------------------------------- plans ----
 
-def plan(coll_kind, p, rank, count, dtype, op, root=0, recvcnts=None, opkind=None):
-    """Rank `rank`'s plan; opkind (OPKIND_*) for a user op, None = predefined."""
+def plan(coll_kind, p, rank, count, dtype, op, root=0, recvcnts=None, opkind=None, tuning=None):
+    """Rank `rank`'s plan; opkind (OPKIND_*) for a user op, None = predefined;
+    tuning (a Tuning) for the device flavour, None = ch_shmem."""
     P = Plan()
     rc_arr = None
     if recvcnts is not None:
         rc_arr = (ctypes.c_int * p)(*recvcnts)
-    if opkind is None:
+    if tuning is not None:
+        rc = coll().mvx_plan_build_tuned(ctypes.byref(P), coll_kind, p, rank, count, rc_arr, dtype, op, root,
+                                         opkind or 0, ctypes.byref(tuning))
+    elif opkind is None:
         rc = coll().mvx_plan_build(ctypes.byref(P), coll_kind, p, rank, count, rc_arr, dtype, op, root)
     else:
         rc = coll().mvx_plan_build_kind(ctypes.byref(P), coll_kind, p, rank, count, rc_arr, dtype, op, root,
@@ -173,10 +192,31 @@ def plan(coll_kind, p, rank, count, dtype, op, root=0, recvcnts=None, opkind=Non
     return P
 
 
-def algorithm(coll_kind, p, total, dtype, opkind=None):
+def algorithm(coll_kind, p, total, dtype, opkind=None, tuning=None):
+    if tuning is not None:
+        return coll().mvx_plan_algorithm_tuned(coll_kind, p, total, dtype, opkind or 0, ctypes.byref(tuning))
     if opkind is None:
         return coll().mvx_plan_algorithm(coll_kind, p, total, dtype)
     return coll().mvx_plan_algorithm_kind(coll_kind, p, total, dtype, opkind)
+
+
+def tuning_from_env(smp=True):
+    """mvx_tuning_from_env: the knobs of an _SMP_ (smp) or ch_shmem build
+    after the VIADEV_* environment.  Raises if the reference would exit."""
+    t = Tuning()
+    rc = coll().mvx_tuning_from_env(ctypes.byref(t), int(bool(smp)))
+    if rc:
+        raise ValueError("mvx_tuning_from_env rc=%d" % rc)
+    return t
+
+
+def smp_tuning(**knobs):
+    """An _SMP_-flavour Tuning with the reference defaults, fields overridden
+    by keyword (e.g. shmem_coll_allreduce_threshold=4096)."""
+    t = Tuning(1, 1, 1, 0, 0, 1 << 10, 1 << 15)
+    for k, v in knobs.items():
+        setattr(t, k, v)
+    return t
 
 
 def dtype_info(dtype):

@@ -123,6 +123,18 @@ class Comm:
     def reserve(self, nbytes):
         return coll().mvx_comm_reserve(self.handle, nbytes)
 
+    def get_tuning(self):
+        """The communicator's device flavour and knobs (a Tuning)."""
+        from . import Tuning
+        t = Tuning()
+        rc = coll().mvx_comm_get_tuning(self.handle, ctypes.byref(t))
+        if rc:
+            raise RuntimeError("mvx_comm_get_tuning rc=%d" % rc)
+        return t
+
+    def set_tuning(self, tuning):
+        return coll().mvx_comm_set_tuning(self.handle, ctypes.byref(tuning))
+
     # stream-ordered (device buffers)
     def allreduce_async(self, sendbuf, recvbuf, count, dtype, op, stream=None):
         return coll().mvx_allreduce_async(addr(sendbuf), addr(recvbuf), count, dtype, op, self.handle,

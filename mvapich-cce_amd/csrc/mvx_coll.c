@@ -67,6 +67,8 @@ typedef struct {
     size_t upool_bytes;
     char *uhost;         /* user-op scratch: pinned host (MPI_User_functions) */
     size_t uhost_bytes;
+    mvx_tuning tune;     /* device flavour + knobs (mvx_coll.h) */
+    int shmem_block;     /* claimed shmem collective block, -1 = none */
 } mvx_comm_t;
 
 static mvx_comm_t g_comms[MAX_COMMS];
@@ -96,6 +98,83 @@ static mvx_comm_t *new_comm(MPI_Comm *out)
     return NULL;
 }
 
+/* ---- device flavour (mvx_tuning) --------------------------------------- */
+
+static int env_int(const char *name, int *out)
+{
+    const char *v = getenv(name);
+    if (!v) return 0;
+    *out = atoi(v);
+    return 1;
+}
+
+/* MPIR_Init's knob parsing for the _SMP_ devices, initutil.c:230-293 */
+int mvx_tuning_from_env(mvx_tuning *t, int smp)
+{
+    int v, max_msg = 1 << 16;   /* shmem_coll_max_msg_size, mpid/ch_gen2/shmem_coll.c:47 */
+    if (!t) return MPI_ERR_ARG;
+    memset(t, 0, sizeof *t);
+    t->shmem_coll_reduce_threshold = 1 << 10;      /* intra_fns_new.c:70-71 */
+    t->shmem_coll_allreduce_threshold = 1 << 15;
+    t->smp = smp ? 1 : 0;
+    if (!t->smp) return MPI_SUCCESS;
+    t->enable_shmem_collectives = 1;               /* initutil.c:146 */
+    t->shmem_coll_ok = 1;
+    if (env_int("VIADEV_USE_SHMEM_REDUCE", &v)) t->disable_shmem_reduce = !v;
+    if (env_int("VIADEV_USE_SHMEM_ALLREDUCE", &v)) t->disable_shmem_allreduce = !v;
+    if (env_int("VIADEV_USE_BLOCKING", &v) && v == 1) t->enable_shmem_collectives = 0;
+    if (env_int("VIADEV_USE_SHMEM_COLL", &v) && v == 0) t->enable_shmem_collectives = 0;
+    if (env_int("VIADEV_USE_SHARED_MEM", &v) && v == 0) t->enable_shmem_collectives = 0;
+    if (env_int("MV_USE_SHARED_MEM", &v) && v == 0) t->enable_shmem_collectives = 0;
+    env_int("VIADEV_SHMEM_COLL_MAX_MSG_SIZE", &max_msg);
+    env_int("VIADEV_SHMEM_COLL_REDUCE_THRESHOLD", &t->shmem_coll_reduce_threshold);
+    env_int("VIADEV_SHMEM_COLL_ALLREDUCE_THRESHOLD", &t->shmem_coll_allreduce_threshold);
+    /* the reference prints "Shmem_coll_max_msg_size should be greater than
+     * the thresholds" and exits (289-293); here the init call fails */
+    if (max_msg < t->shmem_coll_reduce_threshold || max_msg < t->shmem_coll_allreduce_threshold)
+        return MPI_ERR_OTHER;
+    if (!t->enable_shmem_collectives) t->shmem_coll_ok = 0;
+    return MPI_SUCCESS;
+}
+
+/* shmem collective blocks: every _SMP_ communicator's leader takes the first
+ * free one of shmem_coll_blocks (create_2level_comm.c:199-225; 16 by default,
+ * VIADEV_MAX_SHMEM_COLL_COMM, initutil.c:260-266) and frees it with the comm
+ * (free_2level_comm, :96-100). */
+#define MAX_SHMEM_BLOCKS 1024
+static unsigned char g_shmem_taken[MAX_SHMEM_BLOCKS];
+
+static int claim_shmem_block(void)
+{
+    int n = 16, i;
+    env_int("VIADEV_MAX_SHMEM_COLL_COMM", &n);
+    if (n > MAX_SHMEM_BLOCKS) n = MAX_SHMEM_BLOCKS;
+    for (i = 0; i < n; i++)
+        if (!g_shmem_taken[i]) { g_shmem_taken[i] = 1; return i; }
+    return -1;
+}
+
+/* a new communicator's flavour: MVX_DEVICE names the reference device */
+static int comm_flavour(mvx_comm_t *c)
+{
+    const char *d = getenv("MVX_DEVICE");
+    const int smp = d && (!strcmp(d, "ch_gen2") || !strcmp(d, "ch_smp") || !strcmp(d, "ch_gen2_ud"));
+    int rc = mvx_tuning_from_env(&c->tune, smp);
+    c->shmem_block = -1;
+    if (rc) return rc;
+    if (c->tune.smp && c->tune.enable_shmem_collectives) {
+        c->shmem_block = claim_shmem_block();
+        c->tune.shmem_coll_ok = c->shmem_block >= 0;
+    }
+    return MPI_SUCCESS;
+}
+
+static void release_shmem_block(mvx_comm_t *c)
+{
+    if (c->shmem_block >= 0) g_shmem_taken[c->shmem_block] = 0;
+    c->shmem_block = -1;
+}
+
 int mvx_get_unique_id(void *id_out)
 {
     ncclUniqueId id;
@@ -115,8 +194,10 @@ int mvx_comm_init(MPI_Comm *comm, int rank, int size, int device,
     c = new_comm(comm);
     if (!c) return MPI_ERR_INTERN;
     c->rank = rank; c->size = size; c->device = device; c->local = 0;
+    if (comm_flavour(c)) { c->used = 0; return MPI_ERR_OTHER; }
     memcpy(&id, unique_id, MVX_UNIQUE_ID_BYTES);
     if (ncclCommInitRank(&c->nccl, size, id, rank) != ncclSuccess) {
+        release_shmem_block(c);
         c->used = 0;
         return MPI_ERR_OTHER;
     }
@@ -131,6 +212,7 @@ int mvx_comm_init_local(MPI_Comm *comm, int size, int device)
     c = new_comm(comm);
     if (!c) return MPI_ERR_INTERN;
     c->rank = 0; c->size = size; c->device = device; c->local = 1;
+    if (comm_flavour(c)) { c->used = 0; return MPI_ERR_OTHER; }
     return MPI_SUCCESS;
 }
 
@@ -143,6 +225,7 @@ int mvx_comm_free(MPI_Comm *comm)
     if (c->hpool) hipFree(c->hpool);
     if (c->upool) hipFree(c->upool);
     if (c->uhost) hipHostFree(c->uhost);
+    release_shmem_block(c);
     if (c->handle == MPI_COMM_WORLD) g_have_world = 0;
     memset(c, 0, sizeof *c);
     *comm = 0;
@@ -162,6 +245,26 @@ int MPI_Comm_rank(MPI_Comm comm, int *rank)
     mvx_comm_t *c = get_comm(comm);
     if (!c) return ERR_COMM_NULL_CODE;
     *rank = c->rank;
+    return MPI_SUCCESS;
+}
+
+int mvx_comm_get_tuning(MPI_Comm comm, mvx_tuning *t)
+{
+    mvx_comm_t *c = get_comm(comm);
+    if (!c) return ERR_COMM_NULL_CODE;
+    if (!t) return MPI_ERR_ARG;
+    *t = c->tune;
+    return MPI_SUCCESS;
+}
+
+/* Replaces the communicator's flavour and knobs as given (the shmem block
+ * accounting stays with the communicator's creation-time claim). */
+int mvx_comm_set_tuning(MPI_Comm comm, const mvx_tuning *t)
+{
+    mvx_comm_t *c = get_comm(comm);
+    if (!c) return ERR_COMM_NULL_CODE;
+    if (!t) return MPI_ERR_ARG;
+    c->tune = *t;
     return MPI_SUCCESS;
 }
 
@@ -606,8 +709,8 @@ static int run(mvx_comm_t *c, const call_t *k, hipStream_t st, int blocking)
 
     if (c->local) return MPI_ERR_COMM;   /* virtual comms use *_multi */
     mvx_dtype_info(k->dt, &e, &ts);
-    rc = mvx_plan_build_kind(&P, k->coll, c->size, c->rank, k->count, k->recvcnts,
-                             k->dt, k->op, k->root, op_kind(k->op));
+    rc = mvx_plan_build_tuned(&P, k->coll, c->size, c->rank, k->count, k->recvcnts,
+                              k->dt, k->op, k->root, op_kind(k->op), &c->tune);
     if (rc) return rc;
     if (P.alg == MVX_ALG_NONE) return MPI_SUCCESS;
     verdict = op_verdict(k->op, k->dt);
@@ -828,7 +931,8 @@ static int run_multi(mvx_comm_t *c, int coll, void *const *sendbufs,
     for (r = 0; r < p; r++) rcs[r] = 0;
     if (!predefined(op) && !user_op(op)) { for (r = 0; r < p; r++) rcs[r] = MPI_ERR_OP; return MPI_SUCCESS; }
     for (r = 0; r < p; r++) {
-        rc = mvx_plan_build_kind(&plans[r], coll, p, r, count, recvcnts, dt, op, root, op_kind(op));
+        rc = mvx_plan_build_tuned(&plans[r], coll, p, r, count, recvcnts, dt, op, root, op_kind(op),
+                                  &c->tune);
         if (rc) return rc;
     }
     if (plans[0].alg == MVX_ALG_NONE) return MPI_SUCCESS;

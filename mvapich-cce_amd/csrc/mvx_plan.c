@@ -139,6 +139,32 @@ int mvx_plan_algorithm(int coll, int p, long total, int dtype)
     return mvx_plan_algorithm_kind(coll, p, total, dtype, MVX_OPKIND_PREDEFINED);
 }
 
+/* intra_shmem_Allreduce / intra_shmem_Reduce take their leader path when
+ * (5849-5854, 5066-5070) the comm holds a shmem block, the message is short
+ * (`int stride = count*extent`, the reference's int product, 5847 / 5064),
+ * the path is not disabled, the op commutes and shmem collectives are on. */
+static int smp_leader_path(int coll, long total, int extent, int kind, const mvx_tuning *t)
+{
+    int stride;
+    if (!t || !t->smp || !t->enable_shmem_collectives || !t->shmem_coll_ok) return 0;
+    if (kind == MVX_OPKIND_USER_NONCOMMUTE) return 0;
+    stride = imul32(total, extent);
+    if (coll == MVX_COLL_ALLREDUCE)
+        return !t->disable_shmem_allreduce && stride < t->shmem_coll_allreduce_threshold;
+    if (coll == MVX_COLL_REDUCE)
+        return !t->disable_shmem_reduce && stride < t->shmem_coll_reduce_threshold;
+    return 0;
+}
+
+int mvx_plan_algorithm_tuned(int coll, int p, long total, int dtype, int kind,
+                             const mvx_tuning *t)
+{
+    int e, ts;
+    if (mvx_dtype_info(dtype, &e, &ts) || p < 1 || total <= 0) return MVX_ALG_NONE;
+    if (smp_leader_path(coll, total, e, kind, t)) return MVX_ALG_SMP_LEADER;
+    return mvx_plan_algorithm_kind(coll, p, total, dtype, kind);
+}
+
 /* Does the op's result depend on which operand is inout?  For the IEEE
  * compare-select ops, where NaN and +-0 pick an operand by role (coll.h:14-19,
  * global_ops.c:1297-1309), and for every op on the x87 types: an x87 store
@@ -241,7 +267,8 @@ static int rs_halving_calls(int p, int rank, const int *recvcnts)
 }
 
 static int plan_body(mvx_plan *P, int coll, int p, int rank, long count,
-                     const int *recvcnts, int dtype, int op, int root, int kind)
+                     const int *recvcnts, int dtype, int op, int root, int kind,
+                     const mvx_tuning *t)
 {
     /* noncommutative user ops: every combine is uop(in = lower ranks,
      * inout = higher ranks) (5610-5624, 4922-4936, 6660-6682,
@@ -267,12 +294,38 @@ static int plan_body(mvx_plan *P, int coll, int p, int rank, long count,
         count = total;
     }
     P->count = count;
-    P->alg = mvx_plan_algorithm_kind(coll, p, count, dtype, kind);
+    P->alg = mvx_plan_algorithm_tuned(coll, p, count, dtype, kind, t);
     if (P->alg == MVX_ALG_NONE) return MPI_SUCCESS;   /* nothing to do */
 
     pof2 = pof2_lgn(p, &lgn);
     rem = p - pof2;
     L = log2i(pof2);
+
+    if (P->alg == MVX_ALG_SMP_LEADER) {
+        /* One node: the shmem group is the whole comm in rank order and its
+         * leader is rank 0 (create_2level_comm.c:125-138).  The leader copies
+         * its vector and folds local ranks 1 .. p-1 into it,
+         * (*uop)(in = x_i, inout = acc) (5872-5888, 5089-5112): a left chain
+         * x0 o x1 o ... o x_{p-1}, the same for every element.  Allreduce
+         * broadcasts it (5926): every rank gets every vector in one exchange
+         * and evaluates the chain itself.  Reduce: root gets the vectors
+         * (the leader's hand-off to root, 5127-5181, moves the same bits). */
+        if (coll == MVX_COLL_REDUCE && rank != root) {
+            set_range(&P->a_send[root], 0, count);
+            return MPI_SUCCESS;
+        }
+        for (s = 0; s < p; s++) {
+            if (s == rank) continue;
+            if (coll == MVX_COLL_ALLREDUCE) set_range(&P->a_send[s], 0, count);
+            set_range(&P->a_recv[s], 0, count);
+        }
+        P->shape = MVX_SHAPE_CHAIN;
+        P->has_combine = 1;
+        P->k = p;
+        for (q = 0; q < p; q++) P->leaf[q] = q;
+        P->c_src_off = 0; P->c_cnt = count; P->c_dst_off = 0;
+        return MPI_SUCCESS;
+    }
 
     if (coll == MVX_COLL_ALLREDUCE) {
         const int newrank = rank < 2 * rem ? (rank % 2 ? rank / 2 : -1) : rank - rem;
@@ -437,19 +490,32 @@ static int plan_body(mvx_plan *P, int coll, int p, int rank, long count,
     return MPI_ERR_ARG;
 }
 
-int mvx_plan_build_kind(mvx_plan *P, int coll, int p, int rank, long count,
-                        const int *recvcnts, int dtype, int op, int root, int kind)
+int mvx_plan_build_tuned(mvx_plan *P, int coll, int p, int rank, long count,
+                         const int *recvcnts, int dtype, int op, int root, int kind,
+                         const mvx_tuning *t)
 {
     int rc;
     if (kind < MVX_OPKIND_PREDEFINED || kind > MVX_OPKIND_USER_NONCOMMUTE) return MPI_ERR_ARG;
-    rc = plan_body(P, coll, p, rank, count, recvcnts, dtype, op, root, kind);
+    rc = plan_body(P, coll, p, rank, count, recvcnts, dtype, op, root, kind, t);
     if (rc == MPI_SUCCESS && P->has_combine && P->shape >= 0) {
         P->tree_mask = P->shape == MVX_SHAPE_TREE ? tree_mask(P->k) : 0u;
         P->chain_mask = P->shape == MVX_SHAPE_CHAIN ? chain_mask(P->k) : 0u;
         if (kind == MVX_OPKIND_USER_NONCOMMUTE && P->shape == MVX_SHAPE_TREE)
             P->tree_swap = P->tree_mask;
     }
+    /* the _SMP_ collops test a predefined op with len = 0 on every rank
+     * before choosing a path (5054-5058, 5841-5845): an undefined pair
+     * fails on all ranks, p = 1 included */
+    if (rc == MPI_SUCCESS && t && t->smp && kind == MVX_OPKIND_PREDEFINED &&
+        P->alg != MVX_ALG_NONE && (coll == MVX_COLL_ALLREDUCE || coll == MVX_COLL_REDUCE))
+        P->calls_uop = 1;
     return rc;
+}
+
+int mvx_plan_build_kind(mvx_plan *P, int coll, int p, int rank, long count,
+                        const int *recvcnts, int dtype, int op, int root, int kind)
+{
+    return mvx_plan_build_tuned(P, coll, p, rank, count, recvcnts, dtype, op, root, kind, NULL);
 }
 
 int mvx_plan_build(mvx_plan *P, int coll, int p, int rank, long count,

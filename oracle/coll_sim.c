@@ -177,6 +177,59 @@ int orc_algorithm(int coll, int p, long total_count, int dtype)
 }
 
 /* ---------------------------------------------------------------------- */
+/* _SMP_ builds (ch_gen2 / ch_smp / ch_gen2_ud): collops->Reduce and
+ * ->Allreduce are intra_shmem_Reduce / intra_shmem_Allreduce
+ * (intra_fns_new.c:293-310).  One node: the shmem group is every rank in
+ * rank order, its leader rank 0 (create_2level_comm.c:125-138). */
+static struct {
+    int smp, enable, ok, dis_red, dis_ar, thr_red, thr_ar;
+} g_smp = {0, 1, 1, 0, 0, 1 << 10, 1 << 15};
+
+int orc_smp_set(int smp, int enable, int ok, int dis_red, int dis_ar, int thr_red,
+                int thr_ar)
+{
+    g_smp.smp = smp; g_smp.enable = enable; g_smp.ok = ok;
+    g_smp.dis_red = dis_red; g_smp.dis_ar = dis_ar;
+    g_smp.thr_red = thr_red; g_smp.thr_ar = thr_ar;
+    return 0;
+}
+
+/* the leader-path test of 5066-5070 / 5849-5854 (`int stride = count*extent`) */
+static int smp_leader(int thr, int disabled, int count, int E, int op)
+{
+    return g_smp.ok && imul32(count, E) < thr && !disabled && commute(op) && g_smp.enable;
+}
+
+/* The leader's gather-and-fold: tmpbuf = a copy of its own sendbuf (5872),
+ * every other local rank copies its sendbuf into its shmem slot (5918), and
+ * the leader calls (*uop)(slot i, tmpbuf) for i = 1 .. local_size-1
+ * (5885-5888; Reduce 5089-5112). */
+static char *smp_fold(int p, const void *const *send, int count, int dtype, int op)
+{
+    int E, TS, i, dummy = 0;
+    long bytes;
+    char *tmp;
+    orc_dtype_info(dtype, &E, &TS);
+    bytes = (long)count * E;
+    tmp = (char *)calloc((size_t)bytes + 1, 1);
+    tm_copy(tmp, send[0], count, dtype);
+    for (i = 1; i < p; i++) {
+        char *slot = (char *)calloc((size_t)bytes + 1, 1);
+        tm_copy(slot, send[i], count, dtype);
+        uop(op, dtype, slot, tmp, count, &dummy);
+        free(slot);
+    }
+    return tmp;
+}
+
+/* the len = 0 test every rank makes first for a predefined op (5841-5845,
+ * 5054-5058); returns its MPIR_Op_errno */
+static int smp_precheck(int op, int dtype, const void *send, void *recv)
+{
+    return permanent(op) ? orc_op(op, dtype, send, recv, 0) : 0;
+}
+
+/* ---------------------------------------------------------------------- */
 
 int orc_allreduce(int p, const void *const *send, void *const *recv,
                   int count, int dtype, int op, int *rc)
@@ -195,6 +248,21 @@ int orc_allreduce(int p, const void *const *send, void *const *recv,
     if (count < 0) { for (r = 0; r < p; r++) rc[r] = ERR_COUNT; return 0; }
     if (count == 0) return 0;
     if (!op_valid(op)) { for (r = 0; r < p; r++) rc[r] = ERR_OP; return 0; }
+
+    if (g_smp.smp) {   /* intra_shmem_Allreduce, intra_fns_new.c:5793-5940 */
+        int e = smp_precheck(op, dtype, send[0], recv[0]);
+        if (e) { for (r = 0; r < p; r++) rc[r] = e; return 0; }
+        if (smp_leader(g_smp.thr_ar, g_smp.dis_ar, count, E, op)) {
+            if (p == 1) tm_copy(recv[0], send[0], count, dtype);          /* 5909-5911 */
+            else {
+                char *tmp = smp_fold(p, send, count, dtype, op);
+                tm_copy(recv[0], tmp, count, dtype);                       /* 5904-5906 */
+                free(tmp);
+                for (r = 1; r < p; r++) tm_copy(recv[r], recv[0], count, dtype);  /* Bcast 5926 */
+            }
+            return 0;
+        }
+    }
 
     bytes = (long)count * E;
     newrank = (int *)calloc((size_t)p, sizeof(int));
@@ -341,6 +409,22 @@ int orc_reduce(int p, const void *const *send, void *const *recv,
     if (count == 0) return 0;
     if (root < 0 || root >= p) { for (r = 0; r < p; r++) rc[r] = 7; return 0; }
     if (!op_valid(op)) { for (r = 0; r < p; r++) rc[r] = ERR_OP; return 0; }
+
+    if (g_smp.smp) {   /* intra_shmem_Reduce, intra_fns_new.c:4992-5198 */
+        int e = smp_precheck(op, dtype, send[0], recv[0]);
+        if (e) { for (r = 0; r < p; r++) rc[r] = e; return 0; }
+        if (smp_leader(g_smp.thr_red, g_smp.dis_red, count, E, op)) {
+            if (p == 1) tm_copy(recv[root], send[0], count, dtype);       /* 5135-5137 */
+            else {
+                /* root 0: the leader copies tmpbuf into recvbuf (5129-5131);
+                 * otherwise it sends tmpbuf to root (5168-5171, 5179-5181) */
+                char *tmp = smp_fold(p, send, count, dtype, op);
+                tm_copy(recv[root], tmp, count, dtype);
+                free(tmp);
+            }
+            return 0;
+        }
+    }
 
     bytes = (long)count * E;
     err = (int *)calloc((size_t)p, sizeof(int));

@@ -60,6 +60,16 @@ int orc_user_op_set(int handle, orc_user_fn *fn, int commute);
 /* orc_op for any handle, user ops included */
 int orc_call(int op, int dtype, const void *in, void *inout, int len);
 
+/* Device flavour of the replays.  smp = 0 (default): the ch_shmem build's
+ * collops (intra_Reduce / intra_Allreduce).  smp = 1: the _SMP_ builds'
+ * intra_shmem_Reduce / intra_shmem_Allreduce (intra_fns_new.c:4992-5198,
+ * 5793-5940) on one node -- the len = 0 op test on every rank, then the
+ * leader's rank-order fold below the thresholds (bytes, `count*extent`),
+ * with the knobs enable_shmem_collectives, shmem_coll_ok,
+ * disable_shmem_reduce / _allreduce. */
+int orc_smp_set(int smp, int enable, int ok, int dis_red, int dis_ar, int thr_red,
+                int thr_ar);
+
 /* MPI_Scan, the default MPIR_intra_Scan (intra_scan.c:91-150) */
 int orc_scan(int p, const void *const *send, void *const *recv, int count,
              int dtype, int op, int *rc);

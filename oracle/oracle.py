@@ -48,6 +48,7 @@ def lib():
         L.orc_algorithm.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_long, ctypes.c_int]
         L.orc_algorithm_op.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_long, ctypes.c_int, ctypes.c_int]
         L.orc_user_op_set.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
+        L.orc_smp_set.argtypes = [ctypes.c_int] * 7
         L.orc_fill.argtypes = [vp, ctypes.c_long, ctypes.c_int, ctypes.c_int]
         L.orc_fill.restype = None
         _lib = L
@@ -117,6 +118,33 @@ def algorithm(coll, p, total_count, dtype, op=None):
 def user_op_set(handle, fn_addr, commute):
     """Register an MPI_User_function (C address) as user op `handle` (200..263)."""
     return lib().orc_user_op_set(handle, fn_addr, commute)
+
+
+SMP_DEFAULTS = dict(enable=1, ok=1, dis_red=0, dis_ar=0, thr_red=1 << 10, thr_ar=1 << 15)
+
+
+def smp_set(smp, **knobs):
+    """Replay the _SMP_ builds' intra_shmem_* collops (smp=1) or the ch_shmem
+    build's (smp=0).  knobs: enable, ok, dis_red, dis_ar, thr_red, thr_ar."""
+    k = dict(SMP_DEFAULTS)
+    k.update(knobs)
+    return lib().orc_smp_set(int(smp), k["enable"], k["ok"], k["dis_red"], k["dis_ar"], k["thr_red"],
+                             k["thr_ar"])
+
+
+class smp_flavour:
+    """Context manager: the oracle replays the _SMP_ collops inside."""
+
+    def __init__(self, **knobs):
+        self.knobs = knobs
+
+    def __enter__(self):
+        smp_set(1, **self.knobs)
+        return self
+
+    def __exit__(self, *exc):
+        smp_set(0)
+        return False
 
 
 def fill(nbytes_or_array, n, dist, rank):
