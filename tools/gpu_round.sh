@@ -12,7 +12,7 @@ if [[ $STAGE == all || $STAGE == smoke ]]; then
   tail -2 gpurun_out/smoke.log
 fi
 if [[ $STAGE == all || $STAGE == test ]]; then
-  run timeout -k 10 1500 python -m pytest tests -m gpu -x -q -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1 || { tail -60 gpurun_out/pytest_gpu.log; exit 1; }
+  run timeout -k 10 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { tail -60 gpurun_out/pytest_gpu.log; exit 1; }
   tail -3 gpurun_out/pytest_gpu.log
 fi
 if [[ $STAGE == all || $STAGE == bench ]]; then
