@@ -62,6 +62,20 @@ int MPI_Scan(void *sendbuf, void *recvbuf, int count, MPI_Datatype datatype,
 int MPI_Op_create(MPI_User_function *function, int commute, MPI_Op *op);
 int MPI_Op_free(MPI_Op *op);
 
+/* Derived datatypes, contiguous only (include/mpi.h:369-385;
+ * src/pt2pt/type_contig.c, type_commit.c, type_free.c, type_extent.c,
+ * type_size.c): usable with every collective here -- with MPI_Op_create ops
+ * (the user function gets the derived handle, as in the reference), and with
+ * MPI_MAXLOC / MPI_MINLOC when the type is a count-2 contiguous pair over
+ * INT, LONG, LONG_LONG_INT, SHORT, CHAR, FLOAT, DOUBLE or LONG_DOUBLE
+ * (global_ops.c:1387-1503 / 1625-1740); any other predefined op on a derived
+ * type is the reference's 329.  Table in libmvx_hip.so (mvx_hip.h). */
+int MPI_Type_contiguous(int count, MPI_Datatype oldtype, MPI_Datatype *newtype);
+int MPI_Type_commit(MPI_Datatype *datatype);
+int MPI_Type_free(MPI_Datatype *datatype);
+int MPI_Type_extent(MPI_Datatype datatype, MPI_Aint *extent);
+int MPI_Type_size(MPI_Datatype datatype, int *size);
+
 /* A user op whose function runs on the device: `function` enqueues
  * inoutvec[i] = invec[i] op inoutvec[i], i < len, on `stream` (a
  * hipStream_t) and returns 0, or nonzero to fail the call.  Collectives give

@@ -50,10 +50,31 @@ int mvx_op_supported(int op, int dtype);
 /* Bytes per element (the datatype extent) on the device path, or 0. */
 int mvx_dtype_extent(int dtype);
 
+/* Derived datatypes: MPI_Type_contiguous (src/pt2pt/type_contig.c:52-187).
+ * A contiguous type over a contiguous type that has an old type (MPI_2INT or
+ * another derived contiguous type) is flattened as the reference does
+ * (:139-146): contig(1, MPI_2INT) is contig(2, MPI_INT).  The ops follow
+ * global_ops.c: only MAXLOC / MINLOC on a count-2 contiguous type over INT,
+ * LONG, LONG_LONG_INT, SHORT, CHAR, FLOAT, DOUBLE or LONG_DOUBLE are defined
+ * (stride-2 {value, loc} pairs of the base type, 1387-1503 / 1625-1740);
+ * every other (op, derived type) is 329, as each op's `switch (dte_type)`
+ * has no MPIR_CONTIG case.  Handles are MVX_TYPE_DERIVED_BASE + slot. */
+#define MVX_TYPE_DERIVED_BASE 256
+#define MVX_TYPE_DERIVED_MAX  256
+/* 0, MPI_ERR_COUNT (count < 0), 323 (null or unknown oldtype),
+ * MPI_ERR_TYPE (MPI_LB / MPI_UB), MPI_ERR_INTERN (table full) */
+int mvx_type_contiguous(int count, int oldtype, int *newtype);
+/* 0 (and *type = MPI_DATATYPE_NULL), 323 (null / unknown), 579 (predefined) */
+int mvx_type_free(int *type);
+/* Any handle, basic or derived: its old type after flattening (the handle
+ * itself for a basic type; MPI_INT for MPI_2INT), replication count (1 for
+ * a basic type), extent and size in bytes.  0 or MPI_ERR_TYPE. */
+int mvx_type_describe(int type, int *oldtype, int *count, long *extent, long *size);
+
 /* inout[i] = in[i] op inout[i], i < n.  Returns MPI_SUCCESS, 329 for an
  * undefined (op, type) pair (as MPIR_ERR_OP_NOT_DEFINED), MPI_ERR_OP for an
- * unknown op handle, MPI_ERR_TYPE for a datatype with no device
- * representation (MPI_LONG_DOUBLE, MPI_LONG_DOUBLE_INT). */
+ * unknown op handle.  MPI_LONG_DOUBLE / MPI_LONG_DOUBLE_INT and the
+ * long-double pairs run an integer emulation of the x87 (mvx_xf80.h). */
 int mvx_op_apply(int op, int dtype, const void *in, void *inout, size_t n,
                  void *hip_stream);
 

@@ -23,11 +23,13 @@ extern "C" {
 typedef int MPI_Datatype;
 typedef int MPI_Op;
 typedef int MPI_Comm;
+typedef long MPI_Aint;      /* x86-64 LP64, the reference build's address int */
 
 #define MPI_COMM_WORLD 91   /* reference include/mpi.h:119-120 */
 #define MPI_COMM_SELF  92
 
-/* Datatypes: reference include/mpi.h:64-115 */
+/* Datatypes: reference include/mpi.h:64-115 (MPI_DATATYPE_NULL :158) */
+#define MPI_DATATYPE_NULL      ((MPI_Datatype)0)
 #define MPI_CHAR               ((MPI_Datatype)1)
 #define MPI_UNSIGNED_CHAR      ((MPI_Datatype)2)
 #define MPI_BYTE               ((MPI_Datatype)3)
@@ -42,6 +44,9 @@ typedef int MPI_Comm;
 #define MPI_LONG_DOUBLE        ((MPI_Datatype)12)
 #define MPI_LONG_LONG_INT      ((MPI_Datatype)13)
 #define MPI_LONG_LONG          ((MPI_Datatype)13)
+#define MPI_PACKED             ((MPI_Datatype)14)
+#define MPI_LB                 ((MPI_Datatype)15)
+#define MPI_UB                 ((MPI_Datatype)16)
 #define MPI_FLOAT_INT          ((MPI_Datatype)17)
 #define MPI_DOUBLE_INT         ((MPI_Datatype)18)
 #define MPI_LONG_INT           ((MPI_Datatype)19)
@@ -91,6 +96,10 @@ typedef int MPI_Comm;
  * kinds from mpi_error.h:176,199 */
 #define MVX_ERR_OP_NULL        MVX_ERRCLASS_TO_CODE(MPI_ERR_OP, 3)
 #define MVX_ERR_PERM_OP        MVX_ERRCLASS_TO_CODE(MPI_ERR_ARG, 13)
+/* MPIR_TEST_DTYPE of a null / unknown handle (mpid/ch2/datatype.h:64-65) and
+ * MPI_Type_free of a predefined type (type_free.c:93-96); mpi_error.h:137-139 */
+#define MVX_ERR_TYPE_NULL      MVX_ERRCLASS_TO_CODE(MPI_ERR_TYPE, 5)
+#define MVX_ERR_PERM_TYPE      MVX_ERRCLASS_TO_CODE(MPI_ERR_TYPE, 9)
 
 /* User combination function: inoutvec[i] = invec[i] op inoutvec[i]
  * (reference include/mpi.h:206, opcreate.c:47). */

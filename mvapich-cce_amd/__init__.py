@@ -145,6 +145,15 @@ def _load():
     c.mvx_plan_build_tuned.argtypes = [ctypes.POINTER(Plan), i, i, i, ctypes.c_long, pi, i, i, i, i, pt]
     c.mvx_plan_algorithm_tuned.argtypes = [i, i, ctypes.c_long, i, i, pt]
     c.mvx_tuning_from_env.argtypes = [pt, i]
+    pl = ctypes.POINTER(ctypes.c_long)
+    _hip.mvx_type_contiguous.argtypes = [i, i, pi]
+    _hip.mvx_type_free.argtypes = [pi]
+    _hip.mvx_type_describe.argtypes = [i, pi, pi, pl, pl]
+    c.MPI_Type_contiguous.argtypes = [i, i, pi]
+    c.MPI_Type_commit.argtypes = [pi]
+    c.MPI_Type_free.argtypes = [pi]
+    c.MPI_Type_extent.argtypes = [i, pl]
+    c.MPI_Type_size.argtypes = [i, pi]
     c.mvx_comm_get_tuning.argtypes = [i, pt]
     c.mvx_comm_set_tuning.argtypes = [i, pt]
     for name in ("MPIR_MAXF", "MPIR_MINF", "MPIR_SUM", "MPIR_PROD", "MPIR_LAND", "MPIR_BAND", "MPIR_LOR",

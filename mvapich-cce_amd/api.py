@@ -13,6 +13,7 @@ __all__ = [
     "addr", "stream_handle", "op_apply", "op_combine", "op_program", "Comm",
     "MPI_Allreduce", "MPI_Reduce", "MPI_Reduce_scatter", "MPI_Scan", "MPI_Op_create", "MPI_Op_free", "op_create_device",
     "MPIR_call", "op_errno", "last_kernel", "set_launch",
+    "MPI_Type_contiguous", "MPI_Type_commit", "MPI_Type_free", "MPI_Type_extent", "MPI_Type_size",
 ]
 
 
@@ -237,6 +238,39 @@ def MPI_Op_free(op):
     h = ctypes.c_int(op)
     rc = coll().MPI_Op_free(ctypes.byref(h))
     return rc, h.value
+
+
+def MPI_Type_contiguous(count, oldtype):
+    """Returns (rc, new handle)."""
+    h = ctypes.c_int()
+    rc = coll().MPI_Type_contiguous(count, oldtype, ctypes.byref(h))
+    return rc, h.value
+
+
+def MPI_Type_commit(datatype):
+    h = ctypes.c_int(datatype)
+    return coll().MPI_Type_commit(ctypes.byref(h))
+
+
+def MPI_Type_free(datatype):
+    """Returns (rc, new handle)."""
+    h = ctypes.c_int(datatype)
+    rc = coll().MPI_Type_free(ctypes.byref(h))
+    return rc, h.value
+
+
+def MPI_Type_extent(datatype):
+    """Returns (rc, extent)."""
+    e = ctypes.c_long()
+    rc = coll().MPI_Type_extent(datatype, ctypes.byref(e))
+    return rc, e.value
+
+
+def MPI_Type_size(datatype):
+    """Returns (rc, size)."""
+    s = ctypes.c_int()
+    rc = coll().MPI_Type_size(datatype, ctypes.byref(s))
+    return rc, s.value
 
 
 def MPIR_call(name, invec, inoutvec, length, datatype):

@@ -355,6 +355,39 @@ int mvx_op_create_device(MVX_Device_function *function, int commute, MPI_Op *op)
     return op_register(NULL, function, commute, op);
 }
 
+/* ---- derived datatypes (the table is libmvx_hip.so's) ------------------ */
+
+int MPI_Type_contiguous(int count, MPI_Datatype old, MPI_Datatype *newtype)
+{
+    return mvx_type_contiguous(count, old, newtype);
+}
+
+int MPI_Type_commit(MPI_Datatype *datatype)   /* type_commit.c:41-143 */
+{
+    if (!datatype || mvx_type_describe(*datatype, NULL, NULL, NULL, NULL)) return MVX_ERR_TYPE_NULL;
+    return MPI_SUCCESS;   /* contiguous types need no flattening */
+}
+
+int MPI_Type_free(MPI_Datatype *datatype) { return mvx_type_free(datatype); }
+
+int MPI_Type_extent(MPI_Datatype datatype, MPI_Aint *extent)
+{
+    long e;
+    if (mvx_type_describe(datatype, NULL, NULL, &e, NULL)) return MVX_ERR_TYPE_NULL;
+    if (!extent) return MPI_ERR_ARG;
+    *extent = e;
+    return MPI_SUCCESS;
+}
+
+int MPI_Type_size(MPI_Datatype datatype, int *size)
+{
+    long s;
+    if (mvx_type_describe(datatype, NULL, NULL, NULL, &s)) return MVX_ERR_TYPE_NULL;
+    if (!size) return MPI_ERR_ARG;
+    *size = (int)s;
+    return MPI_SUCCESS;
+}
+
 /* the plan kind of an op handle (an invalid handle plans as predefined and
  * is rejected by op_verdict) */
 static int op_kind(MPI_Op op)

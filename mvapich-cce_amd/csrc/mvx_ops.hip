@@ -53,6 +53,11 @@ struct pli { int64_t v; int32_t l; int32_t pad; };      // 16 B
 struct psi { int16_t v; int16_t pad; int32_t l; };      // 8 B
 struct pii { int32_t v; int32_t l; };                   // MPI_2INT
 static_assert(sizeof(pdi) == 16 && sizeof(pli) == 16 && sizeof(psi) == 8, "");
+// contiguous count-2 types over one base type (MPI_2INT's family, e.g.
+// MPI_Type_contiguous(2, MPI_FLOAT)): value and loc both of the base type,
+// global_ops.c:1387-1503 / 1625-1740
+template <typename B> struct pp { B v; B l; };
+static_assert(sizeof(pp<int8_t>) == 2 && sizeof(pp<double>) == 16, "");
 
 // x87 long double (16-byte slot) and MPI_LONG_DOUBLE_INT (32 bytes):
 // integer emulation of the x87 unit, mvx_xf80.h
@@ -129,7 +134,7 @@ __device__ __forceinline__ T loc_op(T a, T b)
 {
     const bool eq = a.v == b.v;
     const bool take = MIN ? (a.v > b.v) : (a.v < b.v);
-    const int32_t lmin = (a.l > b.l) ? b.l : a.l;
+    const decltype(a.l) lmin = (a.l > b.l) ? b.l : a.l;   // MPIR_MIN, coll.h:14-15
     T r = a;
     r.v = take ? b.v : a.v;
     r.l = eq ? lmin : (take ? b.l : a.l);
@@ -153,6 +158,26 @@ template <> struct F<OLOR, xf80> { static __device__ __forceinline__ xf80 f(xf80
 template <> struct F<OLXOR, xf80> { static __device__ __forceinline__ xf80 f(xf80 a, xf80 b) { return xf::lxor(a, b); } };
 template <> struct F<OMAXLOC, pxi> { static __device__ __forceinline__ pxi f(pxi a, pxi b) { return xf::loc<false>(a, b); } };
 template <> struct F<OMINLOC, pxi> { static __device__ __forceinline__ pxi f(pxi a, pxi b) { return xf::loc<true>(a, b); } };
+
+// contiguous(2, MPI_LONG_DOUBLE) pairs (global_ops.c:1483-1496, 1720-1733):
+// x87 compares of the values; equal -> loc = MPIR_MIN(a.l, b.l) (x87 select);
+// b strictly larger (smaller) -> both of b's 10-byte values.  Each slot's
+// padding stays the inout operand's.
+template <bool MIN>
+__device__ __forceinline__ pp<xf80> xloc2(pp<xf80> a, pp<xf80> b)
+{
+    const int c = xf::cmp(a.v, b.v);
+    pp<xf80> r = a;
+    if (c == 0) {
+        r.l = xf::min(a.l, b.l);
+    } else if (c == (MIN ? 1 : -1)) {
+        r.v = xf::with_bits(a.v, b.v.m, b.v.se);
+        r.l = xf::with_bits(a.l, b.l.m, b.l.se);
+    }
+    return r;
+}
+template <> struct F<OMAXLOC, pp<xf80>> { static __device__ __forceinline__ pp<xf80> f(pp<xf80> a, pp<xf80> b) { return xloc2<false>(a, b); } };
+template <> struct F<OMINLOC, pp<xf80>> { static __device__ __forceinline__ pp<xf80> f(pp<xf80> a, pp<xf80> b) { return xloc2<true>(a, b); } };
 
 // ---------------------------------------------------------------------------
 // launch parameters (passed by value, ~170 bytes of kernarg)
@@ -410,10 +435,74 @@ static KSet kset(const char *name)
 // element kinds of the datatype handles (mvx_mpi.h / reference mpi.h:64-115)
 enum { EK_NONE = 0, EK_I8, EK_U8, EK_BYTE, EK_I16, EK_U16, EK_I32, EK_U32,
        EK_I64, EK_U64, EK_F32, EK_F64, EK_C32, EK_C64, EK_PFI, EK_PDI, EK_PLI,
-       EK_PSI, EK_PII, EK_LDBL, EK_LDBL_INT };
+       EK_PSI, EK_PII, EK_LDBL, EK_LDBL_INT,
+       // derived contiguous types: count-2 pairs of one base, and the rest
+       EK_PP8, EK_PP16, EK_PP64, EK_PPF, EK_PPD, EK_PPX, EK_DERIVED };
+
+// ---------------------------------------------------------------------------
+// derived datatypes (MPI_Type_contiguous, src/pt2pt/type_contig.c:52-187)
+
+struct Derived {
+    int used;
+    int old;         // old type after flattening (a basic or pair handle)
+    int count;       // replication count
+    int is_contig;   // the reference's is_contig (decides later flattening)
+    long extent, size;
+};
+static Derived g_types[MVX_TYPE_DERIVED_MAX];
+
+// the basic and pair handles as MPIR_Init_dtes registers them
+// (initdte.c:106-280): extent, size, is_contig (the pair structs with an
+// MPI_UB past a hole, size != extent, are not contiguous: type_commit.c:67-75)
+static bool basic_info(int dtype, long *e, long *s, int *contig)
+{
+    *contig = 1;
+    switch (dtype) {
+    case MPI_CHAR: case MPI_UNSIGNED_CHAR: case MPI_BYTE: case MPI_PACKED: *e = *s = 1; return true;
+    case MPI_SHORT: case MPI_UNSIGNED_SHORT: *e = *s = 2; return true;
+    case MPI_INT: case MPI_UNSIGNED: case MPI_FLOAT: *e = *s = 4; return true;
+    case MPI_LONG: case MPI_UNSIGNED_LONG: case MPI_DOUBLE: case MPI_LONG_LONG_INT: *e = *s = 8; return true;
+    case MPI_LONG_DOUBLE: *e = *s = 16; return true;
+    case MPI_FLOAT_INT: *e = 8; *s = 8; return true;
+    case MPI_2INT: *e = 8; *s = 8; return true;
+    case MPI_DOUBLE_INT: *e = 16; *s = 12; *contig = 0; return true;
+    case MPI_LONG_INT: *e = 16; *s = 12; *contig = 0; return true;
+    case MPI_SHORT_INT: *e = 8; *s = 6; *contig = 0; return true;
+    case MPI_LONG_DOUBLE_INT: *e = 32; *s = 20; *contig = 0; return true;
+    case MPI_COMPLEX: *e = *s = 8; return true;
+    case MPI_DOUBLE_COMPLEX: *e = *s = 16; return true;
+    default: return false;
+    }
+}
+
+static Derived *derived(int h)
+{
+    const int i = h - MVX_TYPE_DERIVED_BASE;
+    if (i < 0 || i >= MVX_TYPE_DERIVED_MAX || !g_types[i].used) return nullptr;
+    return &g_types[i];
+}
+
+static int derived_kind(const Derived *d)
+{
+    if (d->count != 2) return EK_DERIVED;
+    switch (d->old) {              // the base's dte_type, global_ops.c:1395-1497
+    case MPI_INT: return EK_PII;
+    case MPI_LONG: case MPI_LONG_LONG_INT: return EK_PP64;
+    case MPI_SHORT: return EK_PP16;
+    case MPI_CHAR: return EK_PP8;
+    case MPI_FLOAT: return EK_PPF;
+    case MPI_DOUBLE: return EK_PPD;
+    case MPI_LONG_DOUBLE: return EK_PPX;
+    default: return EK_DERIVED;
+    }
+}
 
 static int ekind(int dtype)
 {
+    if (dtype >= MVX_TYPE_DERIVED_BASE) {
+        const Derived *d = derived(dtype);
+        return d ? derived_kind(d) : EK_NONE;
+    }
     switch (dtype) {
     case MPI_CHAR: return EK_I8;
     case MPI_UNSIGNED_CHAR: return EK_U8;
@@ -437,12 +526,6 @@ static int ekind(int dtype)
     case MPI_LONG_DOUBLE_INT: return EK_LDBL_INT;
     default: return EK_NONE;
     }
-}
-
-static int ek_size(int ek)
-{
-    static const int sz[] = {0, 1, 1, 1, 2, 2, 4, 4, 8, 8, 4, 8, 8, 16, 8, 16, 16, 8, 8, 16, 32};
-    return sz[ek];
 }
 
 // Integer SUM/PROD/logical/bitwise results do not depend on signedness in
@@ -479,6 +562,13 @@ static int ek_size(int ek)
     case EK_LDBL: { static KSet s = kset<O, xf80>(NAME "_f80"); return &s; }
 #define LDBL_INT(O, NAME)                                                    \
     case EK_LDBL_INT: { static KSet s = kset<O, pxi>(NAME "_long_double_int"); return &s; }
+#define CONTIG_PAIRS(O, NAME)                                                \
+    case EK_PP8:  { static KSet s = kset<O, pp<int8_t>>(NAME "_2char"); return &s; } \
+    case EK_PP16: { static KSet s = kset<O, pp<int16_t>>(NAME "_2short"); return &s; } \
+    case EK_PP64: { static KSet s = kset<O, pp<int64_t>>(NAME "_2long"); return &s; } \
+    case EK_PPF:  { static KSet s = kset<O, pp<float>>(NAME "_2float"); return &s; } \
+    case EK_PPD:  { static KSet s = kset<O, pp<double>>(NAME "_2double"); return &s; } \
+    case EK_PPX:  { static KSet s = kset<O, pp<xf80>>(NAME "_2long_double"); return &s; }
 
 // Returns the kernel set, or NULL with *rc set to the reference's answer for
 // that (op, type): 329 where the op's switch has no case for it
@@ -518,10 +608,10 @@ static const KSet *lookup(int op, int dtype, int *rc)
         switch (ek) { case EK_BYTE: ARITH_INT(OBXOR, "bxor") default: return nullptr; }
     case MPI_MAXLOC:
         switch (ek) { PAIRS(OMAXLOC, "maxloc")
-        LDBL_INT(OMAXLOC, "maxloc") default: return nullptr; }
+        LDBL_INT(OMAXLOC, "maxloc") CONTIG_PAIRS(OMAXLOC, "maxloc") default: return nullptr; }
     case MPI_MINLOC:
         switch (ek) { PAIRS(OMINLOC, "minloc")
-        LDBL_INT(OMINLOC, "minloc") default: return nullptr; }
+        LDBL_INT(OMINLOC, "minloc") CONTIG_PAIRS(OMINLOC, "minloc") default: return nullptr; }
     default:
         *rc = MPI_ERR_OP;
         return nullptr;
@@ -596,10 +686,89 @@ extern "C" int mvx_op_supported(int op, int dtype)
     return lookup(op, dtype, &rc) != nullptr;
 }
 
+extern "C" int mvx_type_describe(int type, int *oldtype, int *count, long *extent, long *size)
+{
+    long e, s;
+    int contig, old = type, cnt = 1;
+    if (const Derived *d = derived(type)) {
+        old = d->old; cnt = d->count; e = d->extent; s = d->size;
+    } else if (basic_info(type, &e, &s, &contig)) {
+        if (type == MPI_2INT) { old = MPI_INT; cnt = 2; }   // initdte.c:167
+    } else {
+        return MPI_ERR_TYPE;
+    }
+    if (oldtype) *oldtype = old;
+    if (count) *count = cnt;
+    if (extent) *extent = e;
+    if (size) *size = s;
+    return MPI_SUCCESS;
+}
+
+// type_contig.c:52-187: argument checks (66-75), then the flattening of a
+// contiguous old type that has an old type itself (139-146), extent and size
+// from the old type (149-169)
+extern "C" int mvx_type_contiguous(int count, int oldtype, int *newtype)
+{
+    Derived o, n;
+    long be, bs;   // extent / size of one element of n.old
+    if (!newtype) return MPI_ERR_ARG;
+    if (oldtype == MPI_LB || oldtype == MPI_UB)       // valid handles, refused (70-71)
+        return count < 0 ? MPI_ERR_COUNT : MPI_ERR_TYPE;
+    if (const Derived *d = derived(oldtype)) {
+        o = *d;
+    } else {
+        int c;
+        memset(&o, 0, sizeof o);
+        if (!basic_info(oldtype, &o.extent, &o.size, &c)) return MVX_ERR_TYPE_NULL;   // 66-67
+        o.is_contig = c;
+        o.old = oldtype == MPI_2INT ? MPI_INT : oldtype;      // MPI_2INT = contig(2, INT)
+        o.count = oldtype == MPI_2INT ? 2 : 1;
+    }
+    const bool has_old = derived(oldtype) || oldtype == MPI_2INT;
+    if (count < 0) return MPI_ERR_COUNT;                        // 69
+    memset(&n, 0, sizeof n);
+    n.used = 1;
+    if (count == 0) {                                           // 82-116: empty type
+        n.old = oldtype; n.count = 0; n.is_contig = 1; be = bs = 0;
+    } else if (o.is_contig && has_old) {                        // 139-142: flatten
+        n.old = o.old; n.count = count * o.count; n.is_contig = 1;
+        be = o.count ? o.extent / o.count : 0;
+        bs = o.count ? o.size / o.count : 0;
+    } else {                                                    // 143-146
+        n.old = oldtype; n.count = count; n.is_contig = o.is_contig;
+        be = o.extent; bs = o.size;
+    }
+    n.extent = (long)n.count * be;                              // 151
+    n.size = (long)n.count * bs;                                // 169
+    for (int i = 0; i < MVX_TYPE_DERIVED_MAX; ++i) {
+        if (g_types[i].used) continue;
+        g_types[i] = n;
+        *newtype = MVX_TYPE_DERIVED_BASE + i;
+        return MPI_SUCCESS;
+    }
+    return MPI_ERR_INTERN;
+}
+
+// type_free.c:60-105
+extern "C" int mvx_type_free(int *type)
+{
+    long e, s;
+    int c;
+    if (!type) return MPI_ERR_ARG;
+    Derived *d = derived(*type);
+    if (!d) {
+        if (*type != MPI_DATATYPE_NULL && basic_info(*type, &e, &s, &c)) return MVX_ERR_PERM_TYPE;
+        return MVX_ERR_TYPE_NULL;
+    }
+    memset(d, 0, sizeof *d);
+    *type = MPI_DATATYPE_NULL;
+    return MPI_SUCCESS;
+}
+
 extern "C" int mvx_dtype_extent(int dtype)
 {
-    const int ek = ekind(dtype);
-    return ek == EK_NONE ? 0 : ek_size(ek);
+    long e;
+    return mvx_type_describe(dtype, nullptr, nullptr, &e, nullptr) ? 0 : (int)e;
 }
 
 extern "C" int mvx_op_apply(int op, int dtype, const void *in, void *inout,

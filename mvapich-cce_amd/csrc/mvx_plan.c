@@ -47,30 +47,19 @@ static const int coll_table_flat[3 * 5] = {
 #define REDSCAT_COMMUTATIVE_LONG_MSG 524288   /* intra_fns_new.c:39-40 */
 #define REDSCAT_NONCOMMUTATIVE_SHORT_MSG 512
 
+/* Extent and MPI_Type_size of a handle, basic or derived: the datatype table
+ * lives with the kernels that resolve it (mvx_type_describe, libmvx_hip.so;
+ * initdte.c:106-280 for the basic and pair types -- pair structs carry an
+ * MPI_UB, so their extent includes padding and their size does not --
+ * type_contig.c for MPI_Type_contiguous).  MPI_LB / MPI_UB hold no data and
+ * cannot be reduced. */
 int mvx_dtype_info(int dtype, int *extent, int *type_size)
 {
-    int e, s;
-    switch (dtype) {
-    case MPI_CHAR: case MPI_UNSIGNED_CHAR: case MPI_BYTE: case 14: e = s = 1; break;
-    case MPI_SHORT: case MPI_UNSIGNED_SHORT: e = s = 2; break;
-    case MPI_INT: case MPI_UNSIGNED: case MPI_FLOAT: e = s = 4; break;
-    case MPI_LONG: case MPI_UNSIGNED_LONG: case MPI_DOUBLE: case MPI_LONG_LONG_INT:
-        e = s = 8; break;
-    case MPI_LONG_DOUBLE: e = s = 16; break;
-    /* pair structs carry an MPI_UB: extent includes padding, size does not
-       (initdte.c:169-222) */
-    case MPI_FLOAT_INT: e = 8; s = 8; break;
-    case MPI_DOUBLE_INT: e = 16; s = 12; break;
-    case MPI_LONG_INT: e = 16; s = 12; break;
-    case MPI_SHORT_INT: e = 8; s = 6; break;
-    case MPI_2INT: e = 8; s = 8; break;
-    case MPI_LONG_DOUBLE_INT: e = 32; s = 20; break;
-    case MPI_COMPLEX: e = s = 8; break;
-    case MPI_DOUBLE_COMPLEX: e = s = 16; break;
-    default: return MPI_ERR_TYPE;
-    }
-    if (extent) *extent = e;
-    if (type_size) *type_size = s;
+    long e, s;
+    if (mvx_type_describe(dtype, NULL, NULL, &e, &s)) return MPI_ERR_TYPE;
+    if (e > 0x7fffffffL || s > 0x7fffffffL) return MPI_ERR_TYPE;
+    if (extent) *extent = (int)e;
+    if (type_size) *type_size = (int)s;
     return MPI_SUCCESS;
 }
 
@@ -172,7 +161,15 @@ int mvx_plan_algorithm_tuned(int coll, int p, long total, int dtype, int kind,
  * MPI_LONG_DOUBLE's type map moves, stay those of the inout operand. */
 static int op_symmetric(int op, int dtype)
 {
+    int old = dtype, cnt = 1;
     if (dtype == MPI_LONG_DOUBLE || dtype == MPI_LONG_DOUBLE_INT) return 0;
+    if (dtype >= MVX_TYPE_DERIVED_BASE) {
+        /* count-2 contiguous {value, loc} pairs of one base type: the IEEE /
+         * x87 ones pick operands by role (NaN, +-0, slot padding) */
+        mvx_type_describe(dtype, &old, &cnt, NULL, NULL);
+        if (op != MPI_MAXLOC && op != MPI_MINLOC) return 0;
+        return !(old == MPI_FLOAT || old == MPI_DOUBLE || old == MPI_LONG_DOUBLE);
+    }
     switch (op) {
     case MPI_SUM: case MPI_PROD: case MPI_LAND: case MPI_LOR: case MPI_LXOR:
     case MPI_BAND: case MPI_BOR: case MPI_BXOR:

@@ -45,9 +45,88 @@ typedef struct { long v; int l; } p_long_int;     /* initdte.c:86-90 */
 typedef struct { short v; int l; } p_short_int;   /* initdte.c:92-96 */
 typedef struct { long double v; int l; } p_ldouble_int;
 
+/* ---------------------------------------------------------------------- */
+/* Derived contiguous types, restating src/pt2pt/type_contig.c:52-187: a
+ * contiguous old type that has an old type itself (MPI_2INT = contig(2, INT),
+ * or a derived contiguous type) is flattened (139-146); extent and size are
+ * count times the old type's (151, 169).  Handles 256 + slot. */
+#define DT_BASE 256
+#define DT_MAX 256
+static struct { int used, old, count, is_contig; long extent, size; } g_dt[DT_MAX];
+
+static int dt_slot(int h)
+{
+    int i = h - DT_BASE;
+    return (i >= 0 && i < DT_MAX && g_dt[i].used) ? i : -1;
+}
+
+static int basic_contig(int dtype)   /* structs with a hole are not contiguous */
+{
+    return !(dtype == T_DOUBLE_INT || dtype == T_LONG_INT || dtype == T_SHORT_INT ||
+             dtype == T_LDOUBLE_INT);
+}
+
+int orc_type_parts(int dtype, int *old, int *count)
+{
+    int i = dt_slot(dtype);
+    if (i < 0) return ERR_TYPE;
+    *old = g_dt[i].old;
+    *count = g_dt[i].count;
+    return 0;
+}
+
+int orc_type_contiguous(int count, int oldtype, int *newtype)
+{
+    int e, s, i, has_old, o_contig, o_old, o_count, n_old, n_count, n_contig;
+    long be, bs, o_ext, o_size;
+    if (oldtype == T_LB || oldtype == T_UB) return count < 0 ? 2 : ERR_TYPE;
+    if ((i = dt_slot(oldtype)) >= 0) {
+        o_contig = g_dt[i].is_contig; o_old = g_dt[i].old; o_count = g_dt[i].count;
+        o_ext = g_dt[i].extent; o_size = g_dt[i].size; has_old = 1;
+    } else {
+        if (orc_dtype_info(oldtype, &e, &s)) return 3 | (5 << 6);
+        o_contig = basic_contig(oldtype); o_ext = e; o_size = s;
+        has_old = oldtype == T_2INT;
+        o_old = has_old ? T_INT : oldtype; o_count = has_old ? 2 : 1;
+    }
+    if (count < 0) return 2;
+    if (count == 0) {
+        n_old = oldtype; n_count = 0; n_contig = 1; be = bs = 0;
+    } else if (o_contig && has_old) {
+        n_old = o_old; n_count = count * o_count; n_contig = 1;
+        be = o_count ? o_ext / o_count : 0; bs = o_count ? o_size / o_count : 0;
+    } else {
+        n_old = oldtype; n_count = count; n_contig = o_contig; be = o_ext; bs = o_size;
+    }
+    for (i = 0; i < DT_MAX; i++) {
+        if (g_dt[i].used) continue;
+        g_dt[i].used = 1; g_dt[i].old = n_old; g_dt[i].count = n_count;
+        g_dt[i].is_contig = n_contig;
+        g_dt[i].extent = (long)n_count * be; g_dt[i].size = (long)n_count * bs;
+        *newtype = DT_BASE + i;
+        return 0;
+    }
+    return 16;
+}
+
+int orc_type_free(int *dtype)
+{
+    int i = dt_slot(*dtype);
+    if (i < 0) return 3 | (5 << 6);
+    memset(&g_dt[i], 0, sizeof g_dt[i]);
+    *dtype = 0;
+    return 0;
+}
+
 int orc_dtype_info(int dtype, int *extent, int *type_size)
 {
     int e, s;
+    if (dt_slot(dtype) >= 0) {
+        int i = dt_slot(dtype);
+        if (extent) *extent = (int)g_dt[i].extent;
+        if (type_size) *type_size = (int)g_dt[i].size;
+        return 0;
+    }
     switch (dtype) {
     case T_CHAR: case T_UCHAR: case T_BYTE: case T_PACKED: e = s = 1; break;
     case T_SHORT: case T_USHORT: e = s = 2; break;
@@ -151,9 +230,48 @@ static int loc_op(int is_min, int dtype, const void *in, void *inout, int len)
     }
 }
 
+/* MAXLOC / MINLOC on a derived contiguous type with count == 2: stride-2
+ * scalars of the old type (global_ops.c:1387-1503, 1625-1740); len is
+ * doubled (1392).  Any other derived type: 329 (1504-1507, 1741-1744). */
+#define CONTIG2_LOOP(T)                                                      \
+    do {                                                                     \
+        T *a = (T *)inout; const T *b = (const T *)in;                       \
+        for (i = 0; i < n2; i += 2) {                                        \
+            if (a[i] == b[i])                                                \
+                a[i + 1] = (a[i + 1] > b[i + 1]) ? b[i + 1] : a[i + 1];      \
+            else if (is_min ? (a[i] > b[i]) : (a[i] < b[i])) {               \
+                a[i] = b[i];                                                 \
+                a[i + 1] = b[i + 1];                                         \
+            }                                                                \
+        }                                                                    \
+    } while (0)
+
+static int derived_loc_op(int is_min, int dtype, const void *in, void *inout, int len)
+{
+    int old, count, i, n2;
+    if (orc_type_parts(dtype, &old, &count) || count != 2) return ERR_OP_NOT_DEFINED;
+    n2 = len * count;
+    switch (old) {
+    case T_INT:     CONTIG2_LOOP(int); return 0;
+    case T_LONG:    CONTIG2_LOOP(long); return 0;
+    case T_LLONG:   CONTIG2_LOOP(long long); return 0;
+    case T_SHORT:   CONTIG2_LOOP(short); return 0;
+    case T_CHAR:    CONTIG2_LOOP(char); return 0;
+    case T_FLOAT:   CONTIG2_LOOP(float); return 0;
+    case T_DOUBLE:  CONTIG2_LOOP(double); return 0;
+    case T_LDOUBLE: CONTIG2_LOOP(long double); return 0;
+    default: return ERR_OP_NOT_DEFINED;
+    }
+}
+
 int orc_op(int op, int dtype, const void *in, void *inout, int len)
 {
     int i;
+    if (dt_slot(dtype) >= 0) {
+        if (op < 100 || op > 111) return ERR_OP;
+        if (op == 111 || op == 110) return derived_loc_op(op == 110, dtype, in, inout, len);
+        return ERR_OP_NOT_DEFINED;   /* no MPIR_CONTIG case in any other op */
+    }
     switch (op) {
     case 100: /* MPI_MAX */
         switch (dtype) { INT_CASES(E_MAX) FLT_CASES(E_MAX)

@@ -38,6 +38,13 @@ extern "C" {
  * map, excluding padding), or MPI_ERR_TYPE (3) for an unregistered handle. */
 int orc_dtype_info(int dtype, int *extent, int *type_size);
 
+/* MPI_Type_contiguous (type_contig.c:52-187) and MPI_Type_free: derived
+ * handles 256.. usable everywhere a datatype is; orc_type_parts gives the
+ * flattened old type and count.  Codes as the reference (0, 2, 3, 323). */
+int orc_type_contiguous(int count, int oldtype, int *newtype);
+int orc_type_free(int *dtype);
+int orc_type_parts(int dtype, int *old, int *count);
+
 /* One predefined op: inout[i] = in[i] op inout[i] for i < len.
  * Returns 0, or 329 (MPIR_ERR_OP_NOT_DEFINED) for an undefined (op, type)
  * pair (the data is left untouched), or 9 (MPI_ERR_OP) for a bad handle. */

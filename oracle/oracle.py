@@ -49,6 +49,8 @@ def lib():
         L.orc_algorithm_op.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_long, ctypes.c_int, ctypes.c_int]
         L.orc_user_op_set.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
         L.orc_smp_set.argtypes = [ctypes.c_int] * 7
+        L.orc_type_contiguous.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
+        L.orc_type_free.argtypes = [ctypes.POINTER(ctypes.c_int)]
         L.orc_fill.argtypes = [vp, ctypes.c_long, ctypes.c_int, ctypes.c_int]
         L.orc_fill.restype = None
         _lib = L
@@ -118,6 +120,18 @@ def algorithm(coll, p, total_count, dtype, op=None):
 def user_op_set(handle, fn_addr, commute):
     """Register an MPI_User_function (C address) as user op `handle` (200..263)."""
     return lib().orc_user_op_set(handle, fn_addr, commute)
+
+
+def type_contiguous(count, oldtype):
+    """MPI_Type_contiguous in the oracle's own table: (rc, handle)."""
+    h = ctypes.c_int()
+    rc = lib().orc_type_contiguous(count, oldtype, ctypes.byref(h))
+    return rc, h.value
+
+
+def type_free(handle):
+    h = ctypes.c_int(handle)
+    return lib().orc_type_free(ctypes.byref(h))
 
 
 SMP_DEFAULTS = dict(enable=1, ok=1, dis_red=0, dis_ar=0, thr_red=1 << 10, thr_ar=1 << 15)

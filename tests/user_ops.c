@@ -62,6 +62,15 @@ void uop_mix(void *in, void *inout, int *len, int *dt)
     }
 }
 
+/* uop_mix over a derived type of 3 unsigned words (MPI_Type_contiguous(3,
+ * MPI_UNSIGNED)): *len counts derived elements, so 3 * *len words -- the
+ * element-wise contract a user function has with its datatype */
+void uop_mix3(void *in, void *inout, int *len, int *dt)
+{
+    int n = 3 * *len;
+    uop_mix(in, inout, &n, dt);
+}
+
 void uop_affine(void *in, void *inout, int *len, int *dt)
 {
     const uint64_t *a = (const uint64_t *)in;
