@@ -97,6 +97,12 @@ int orc_algorithm_op(int coll, int p, long total_count, int dtype, int op);
 #define ORC_COLL_REDUCE         2
 #define ORC_COLL_REDUCE_SCATTER 3
 
+/* CPU baseline: the reference's schedules run by p
+ * host threads over shared memory (oracle/cpu_coll.c), p a power of two;
+ * Reduce: binomial tree only.  Returns seconds per collective. */
+double orc_threads_coll(int coll, int p, void *const *send, void *const *recv, void *const *tmp,
+                        int count, const int *recvcnts, int dtype, int op, int root, int reps);
+
 /* Synthetic input generator: xorshift64 seeded
  * 0x9E3779B97F4A7C15 ^ (rank*1000003 + 1).  dist: 0 mixed-sign f32,
  * 1 U[0,1) f32, 2 int64 with P(bit)=0.953, 3 FLOAT_INT v=u%1024 l=rank,

@@ -51,6 +51,10 @@ def lib():
         L.orc_smp_set.argtypes = [ctypes.c_int] * 7
         L.orc_type_contiguous.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
         L.orc_type_free.argtypes = [ctypes.POINTER(ctypes.c_int)]
+        L.orc_threads_coll.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp), ctypes.POINTER(vp),
+                                       ctypes.POINTER(vp), ctypes.c_int, ctypes.POINTER(ctypes.c_int),
+                                       ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+        L.orc_threads_coll.restype = ctypes.c_double
         L.orc_fill.argtypes = [vp, ctypes.c_long, ctypes.c_int, ctypes.c_int]
         L.orc_fill.restype = None
         _lib = L
@@ -120,6 +124,15 @@ def algorithm(coll, p, total_count, dtype, op=None):
 def user_op_set(handle, fn_addr, commute):
     """Register an MPI_User_function (C address) as user op `handle` (200..263)."""
     return lib().orc_user_op_set(handle, fn_addr, commute)
+
+
+def threads_coll(coll, sends, recvs, tmps, count, dtype, op, root=0, recvcnts=None, reps=1):
+    """The reference schedule on len(sends) host threads (CPU baseline);
+    returns seconds per collective.  tmps[r] must hold 2 x total elements."""
+    p = len(sends)
+    cn = (ctypes.c_int * p)(*recvcnts) if recvcnts is not None else None
+    return lib().orc_threads_coll(coll, p, _ptrs(sends), _ptrs(recvs), _ptrs(tmps), count, cn, dtype, op, root,
+                                  reps)
 
 
 def type_contiguous(count, oldtype):
