@@ -612,7 +612,12 @@ typedef struct {
 } rank_exec_t;
 
 /* staging layout: one slot per received shard, plus the temporary result
- * of a non-root Reduce; returns the bytes this rank needs */
+ * of a non-root Reduce; returns the bytes this rank needs.  Consecutive
+ * slots are 4 KiB apart beyond their size: back-to-back equal-size shards put
+ * the same chunk of every leaf at the same DRAM interleave position, and the
+ * k-leaf combine then ran 5-6 % slower (tools/tune_combine_layout.py,
+ * profiles/r01/tune_combine_layout.jsonl: 53.9 vs 51.2 us for 8 x 32 MiB). */
+#define SLOT_STAGGER 4096
 static size_t exec_layout(rank_exec_t *X)
 {
     const mvx_plan *P = X->P;
@@ -622,7 +627,10 @@ static size_t exec_layout(rank_exec_t *X)
     int s;
     for (s = 0; s < P->p; s++) {
         X->slot[s] = 0;
-        if (P->a_recv[s].cnt) { X->slot[s] = slot_at(need, like); need = X->slot[s] + P->a_recv[s].cnt * E; }
+        if (P->a_recv[s].cnt) {
+            X->slot[s] = slot_at(need, like);
+            need = X->slot[s] + P->a_recv[s].cnt * E + SLOT_STAGGER;
+        }
     }
     X->tmp_off = 0;
     if (P->c_dst_tmp) { X->tmp_off = slot_at(need, like); need = X->tmp_off + P->c_cnt * E; }

@@ -31,9 +31,16 @@ def run(mvx, name, op, dtype, k, shape, leaf_bytes, sets, reps=20, warm=3):
     n_elems = leaf_bytes // mvx.dtype_info(dtype)[0]
     bufs = []
     for s in range(sets):
-        leaves = [torch.randint(0, 1 << 30, (leaf_bytes // 4,), dtype=torch.int32, device="cuda") for _ in range(k)]
-        if dtype == mvx.MPI_FLOAT:
-            leaves = [(x.float() * 1e-6) for x in leaves]
+        if k > 2:
+            # the executor's staging pool: shard slots back to back, 4 KiB
+            # staggered (mvx_coll.c exec_layout)
+            big = torch.randint(0, 1 << 30, (k * (leaf_bytes + 4096) // 4,), dtype=torch.int32, device="cuda")
+            leaves = [big[q * (leaf_bytes + 4096) // 4:][: leaf_bytes // 4] for q in range(k)]
+        else:
+            leaves = [torch.randint(0, 1 << 30, (leaf_bytes // 4,), dtype=torch.int32, device="cuda")
+                      for _ in range(k)]
+        if dtype == mvx.MPI_FLOAT:          # in place: keeps the slot layout
+            leaves = [x.view(torch.float32).copy_(x.float() * 1e-6) for x in leaves]
         elif dtype in (mvx.MPI_LONG_DOUBLE, mvx.MPI_LONG_DOUBLE_INT):
             leaves = [_x87_values(x, dtype, mvx) for x in leaves]
         dst = torch.empty(leaf_bytes // 4, dtype=torch.int32, device="cuda")
