@@ -108,7 +108,10 @@ int PMPI_Scan(void *, void *, int, MPI_Datatype, MPI_Op, MPI_Comm);
 int PMPI_Op_create(MPI_User_function *, int, MPI_Op *);
 int PMPI_Op_free(MPI_Op *);
 
-/* ---- stream-ordered variants (device buffers only) --------------------- */
+/* ---- stream-ordered variants (device buffers only) ---------------------
+ * Calls on one communicator share its staging pool: issue them on one
+ * stream (as MPI orders a communicator's collectives), or synchronise the
+ * streams between calls. */
 int mvx_reduce_async(const void *sendbuf, void *recvbuf, int count,
                      MPI_Datatype datatype, MPI_Op op, int root, MPI_Comm comm,
                      void *hip_stream);
