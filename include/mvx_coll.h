@@ -241,7 +241,19 @@ typedef struct { long off, cnt; } mvx_range;   /* in elements */
  * the source vectors, written to recvbuf + c_dst_off (c_dst_tmp = 0) or to
  * a temporary (1).  Phase C: send the combine output to the ranks in
  * b_send (destination recvbuf coordinates), receive b_recv ranges into
- * recvbuf. */
+ * recvbuf.
+ *
+ * The combine program is a chain of trees over the leaves (every order of
+ * the reference's collectives has this form, k <= MVX_MAXK):
+ *   bit q of seg_heads starts a segment (bit 0 is always set); each segment
+ *   [q, next head) is reduced as a TREE (include/mvx_hip.h: level by level,
+ *   y[q] = op(y[q], y[q + 2^l])) into its first leaf; then, for every later
+ *   head q in ascending order, y[0] = op(y[0], y[q]).
+ * TREE(k) is seg_heads = 1; CHAIN(k) is every leaf a head; MPI_Scan's
+ * partial sums are a chain over [x_r, tree blocks].  The left operand of a
+ * step is the reference's `inoutvec`.  Up to 8 leaves this is one kernel
+ * launch (mvx_op_program masks); beyond, the executor evaluates trees in
+ * groups of 8 and the chain in windows of 8 -- the same association. */
 typedef struct mvx_plan {
     int coll, alg, p, rank, root, op, dtype, esize;
     int symmetric;      /* result independent of operand roles */
@@ -249,20 +261,26 @@ typedef struct mvx_plan {
     long count;         /* vector elements (Reduce_scatter: total) */
     mvx_range a_send[MVX_MAXP];
     mvx_range a_recv[MVX_MAXP];
-    int has_combine, k, shape, c_dst_tmp;
-    unsigned tree_mask, chain_mask;   /* the combine program (mvx_hip.h) */
+    int has_combine, k, shape, c_dst_tmp;   /* shape: MVX_SHAPE_* or -1 (mixed) */
+    unsigned long long seg_heads;           /* the combine program, see above */
     int leaf[MVX_MAXK];
     int leaf_fold[MVX_MAXK];
     long c_src_off, c_cnt, c_dst_off;
     mvx_range b_send[MVX_MAXP];
     mvx_range b_recv[MVX_MAXP];
     int opkind;                       /* MVX_OPKIND_* */
-    /* steps whose operand roles are exchanged: bit set -> the step is
+    /* steps whose operand roles are exchanged: the step is
      * y = uop(in = y_left, inout = y_right), the reference's noncommutative
-     * "order is not right" branch; bits as in tree_mask / chain_mask.  Only
-     * user ops set them (the device kernels never see a swap). */
-    unsigned tree_swap, chain_swap;
+     * "order is not right" branch.  tree_swap: every tree step; chain_swap
+     * bit q: the chain step at head q.  Only user ops set them (the device
+     * kernels never see a swap). */
+    int tree_swap;
+    unsigned long long chain_swap;
 } mvx_plan;
+
+/* The single-launch masks (mvx_op_program) of a plan's program when
+ * k <= MVX_COMBINE_KMAX; returns 0, or MPI_ERR_ARG for a larger k. */
+int mvx_plan_masks(const mvx_plan *plan, unsigned *tree_mask, unsigned *chain_mask);
 
 /* Builds rank `rank`'s plan; returns 0 or an MPI error class. */
 int mvx_plan_build(mvx_plan *plan, int coll, int p, int rank, long count,

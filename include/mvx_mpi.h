@@ -26,6 +26,7 @@ typedef int MPI_Comm;
 typedef long MPI_Aint;      /* x86-64 LP64, the reference build's address int */
 
 #define MPI_COMM_WORLD 91   /* reference include/mpi.h:119-120 */
+#define MPI_BOTTOM ((void *)0)   /* reference include/mpi.h:179 */
 #define MPI_COMM_SELF  92
 
 /* Datatypes: reference include/mpi.h:64-115 (MPI_DATATYPE_NULL :158) */

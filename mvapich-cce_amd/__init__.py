@@ -59,12 +59,25 @@ class Plan(ctypes.Structure):
         ("symmetric", ctypes.c_int), ("calls_uop", ctypes.c_int), ("count", ctypes.c_long),
         ("a_send", Range * MAXP), ("a_recv", Range * MAXP),
         ("has_combine", ctypes.c_int), ("k", ctypes.c_int), ("shape", ctypes.c_int), ("c_dst_tmp", ctypes.c_int),
-        ("tree_mask", ctypes.c_uint), ("chain_mask", ctypes.c_uint),
+        ("seg_heads", ctypes.c_ulonglong),
         ("leaf", ctypes.c_int * MAXK), ("leaf_fold", ctypes.c_int * MAXK),
         ("c_src_off", ctypes.c_long), ("c_cnt", ctypes.c_long), ("c_dst_off", ctypes.c_long),
         ("b_send", Range * MAXP), ("b_recv", Range * MAXP),
-        ("opkind", ctypes.c_int), ("tree_swap", ctypes.c_uint), ("chain_swap", ctypes.c_uint),
+        ("opkind", ctypes.c_int), ("tree_swap", ctypes.c_int), ("chain_swap", ctypes.c_ulonglong),
     ]
+
+    def masks(self):
+        """(tree_mask, chain_mask) of a <= 8-leaf program (mvx_plan_masks)."""
+        t, c = ctypes.c_uint(), ctypes.c_uint()
+        rc = coll().mvx_plan_masks(ctypes.byref(self), ctypes.byref(t), ctypes.byref(c))
+        if rc:
+            raise ValueError("mvx_plan_masks rc=%d" % rc)
+        return t.value, c.value
+
+    def segments(self):
+        """[(start, end)] of the program's tree segments."""
+        heads = [q for q in range(self.k) if self.seg_heads >> q & 1] + [self.k]
+        return list(zip(heads[:-1], heads[1:]))
 
 
 class Tuning(ctypes.Structure):
@@ -137,6 +150,7 @@ def _load():
     c.mvx_reduce_multi.argtypes = [pvp, pvp, i, i, i, i, i, pi, vp]
     c.mvx_reduce_scatter_multi.argtypes = [pvp, pvp, pi, i, i, i, pi, vp]
     c.mvx_plan_build.argtypes = [ctypes.POINTER(Plan), i, i, i, ctypes.c_long, pi, i, i, i]
+    c.mvx_plan_masks.argtypes = [ctypes.POINTER(Plan), ctypes.POINTER(ctypes.c_uint), ctypes.POINTER(ctypes.c_uint)]
     c.mvx_plan_algorithm.argtypes = [i, i, ctypes.c_long, i]
     c.mvx_plan_build_kind.argtypes = [ctypes.POINTER(Plan), i, i, i, ctypes.c_long, pi, i, i, i, i]
     c.mvx_plan_algorithm_kind.argtypes = [i, i, ctypes.c_long, i, i]

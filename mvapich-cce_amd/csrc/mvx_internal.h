@@ -1,0 +1,15 @@
+/*
+ * mvx_internal.h -- declarations shared by libmvx.so's C sources (not part
+ * of the drop-in surface; that is include/mvx_coll.h).
+ */
+#ifndef MVX_INTERNAL_H
+#define MVX_INTERNAL_H
+
+#include <stddef.h>
+
+/* mvx_host.c */
+int mvx_host_pinned(const void *p);
+void mvx_pcopy(void *dst, const void *src, size_t bytes);
+int mvx_copy_threads(void);
+
+#endif

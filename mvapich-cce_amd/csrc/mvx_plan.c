@@ -184,19 +184,28 @@ static int op_symmetric(int op, int dtype)
     }
 }
 
-/* combine programs (include/mvx_hip.h) */
-static unsigned tree_mask(int k)
+/* the single-launch masks of a chain-of-trees program (include/mvx_coll.h,
+ * include/mvx_hip.h): tree steps of every segment at its leaf offset, a
+ * chain bit at every later segment head */
+int mvx_plan_masks(const mvx_plan *P, unsigned *tree_mask, unsigned *chain_mask)
 {
-    unsigned m = 0;
-    int l, q;
-    for (l = 0; (1 << l) < k && l < 3; ++l)
-        for (q = 0; q + (1 << l) < k; q += 2 << l) m |= 1u << (l * 8 + q);
-    return m;
+    unsigned t = 0, c = 0;
+    int s, e, l, q;
+    if (!P || P->k < 1 || P->k > MVX_COMBINE_KMAX) return MPI_ERR_ARG;
+    for (s = 0; s < P->k; s = e) {
+        for (e = s + 1; e < P->k && !(P->seg_heads >> e & 1ull); e++) ;
+        if (s) c |= 1u << s;
+        for (l = 0; (1 << l) < e - s; l++)
+            for (q = 0; q + (1 << l) < e - s; q += 2 << l) t |= 1u << (l * 8 + s + q);
+    }
+    if (tree_mask) *tree_mask = t;
+    if (chain_mask) *chain_mask = c;
+    return MPI_SUCCESS;
 }
 
-static unsigned chain_mask(int k)
+static unsigned long long all_heads(int k)
 {
-    return k >= 2 ? (unsigned)(((1ull << k) - 1) & ~1ull) : 0u;
+    return k >= 64 ? ~0ull : (1ull << k) - 1;
 }
 
 static void set_range(mvx_range *r, long off, long cnt)
@@ -432,20 +441,17 @@ static int plan_body(mvx_plan *P, int coll, int p, int rank, long count,
         }
         P->has_combine = 1;
         P->leaf[0] = rank;
-        P->tree_mask = 0; P->chain_mask = 0;
+        P->seg_heads = 1ull;
+        /* noncommutative: dst's partial is the aligned block in rank order,
+         * lower ranks as `in` at every tree level; the chain keeps recv as
+         * inout (intra_scan.c:124-137) */
+        P->tree_swap = canon;
         for (l = 0; (1 << l) <= rank; l++) {
             const int dst = rank ^ (1 << l), size_l = 1 << l;
-            int q, ll;
+            int q;
             if (!(rank & (1 << l))) continue;
-            /* noncommutative: dst's partial is the aligned block in rank
-             * order, lower ranks as `in` at every level */
             for (q = 0; q < size_l; q++) P->leaf[pos + q] = canon ? ((dst >> l) << l) + q : dst ^ q;
-            for (ll = 0; (1 << ll) < size_l; ll++)
-                for (q = 0; q + (1 << ll) < size_l; q += 2 << ll) {
-                    P->tree_mask |= 1u << (ll * 8 + pos + q);
-                    if (canon) P->tree_swap |= 1u << (ll * 8 + pos + q);
-                }
-            P->chain_mask |= 1u << pos;
+            P->seg_heads |= 1ull << pos;
             pos += size_l;
         }
         P->k = pos;                /* = rank + 1 */
@@ -469,7 +475,7 @@ static int plan_body(mvx_plan *P, int coll, int p, int rank, long count,
             for (q = 0; q < p; q++) P->leaf[q] = (rank - q + p) % p;
             /* noncommutative: src = rank - q above rank swaps (6487-6498) */
             for (q = 1; q < p; q++)
-                if (canon && q > rank) P->chain_swap |= 1u << q;
+                if (canon && q > rank) P->chain_swap |= 1ull << q;
         } else if (P->alg == MVX_ALG_RS_RECDBL) {
             /* noncommutative recursive doubling (6505-6706): block r ends as
              * the rank-ordered tree, lower ranks as `in` */
@@ -495,10 +501,9 @@ int mvx_plan_build_tuned(mvx_plan *P, int coll, int p, int rank, long count,
     if (kind < MVX_OPKIND_PREDEFINED || kind > MVX_OPKIND_USER_NONCOMMUTE) return MPI_ERR_ARG;
     rc = plan_body(P, coll, p, rank, count, recvcnts, dtype, op, root, kind, t);
     if (rc == MPI_SUCCESS && P->has_combine && P->shape >= 0) {
-        P->tree_mask = P->shape == MVX_SHAPE_TREE ? tree_mask(P->k) : 0u;
-        P->chain_mask = P->shape == MVX_SHAPE_CHAIN ? chain_mask(P->k) : 0u;
+        P->seg_heads = P->shape == MVX_SHAPE_TREE ? 1ull : all_heads(P->k);
         if (kind == MVX_OPKIND_USER_NONCOMMUTE && P->shape == MVX_SHAPE_TREE)
-            P->tree_swap = P->tree_mask;
+            P->tree_swap = 1;
     }
     /* the _SMP_ collops test a predefined op with len = 0 on every rank
      * before choosing a path (5054-5058, 5841-5845): an undefined pair

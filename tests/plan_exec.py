@@ -29,8 +29,9 @@ def chain_mask(k):
 
 
 def run_program(op, dtype, leaves, folds, tmask, cmask, n, tswap=0, cswap=0):
-    """The combine program of include/mvx_hip.h, step by step with the oracle
-    op; a swapped step (user ops) is y_left = uop(in = y_left, inout = y_right)."""
+    """The combine program of include/mvx_hip.h (<= 8 leaves, masks), step by
+    step with the oracle op; a swapped step (user ops) is
+    y_left = uop(in = y_left, inout = y_right)."""
     y = []
     for q, a in enumerate(leaves):
         v = a.copy()
@@ -59,6 +60,34 @@ def run_program(op, dtype, leaves, folds, tmask, cmask, n, tswap=0, cswap=0):
     return y[0]
 
 
+def run_plan_program(P, leaves, folds, n):
+    """A plan's chain-of-trees program (include/mvx_coll.h, any k): every
+    segment's tree level by level, then the chain over the segment heads."""
+    y = []
+    for q, a in enumerate(leaves):
+        v = a.copy()
+        if folds is not None and folds[q] is not None:
+            O.op(P.op, P.dtype, folds[q], v, n)
+        y.append(v)
+    for s, e in P.segments():
+        h = 1
+        while h < e - s:
+            for q in range(s, e - h, 2 * h):
+                if P.tree_swap:
+                    O.op(P.op, P.dtype, y[q], y[q + h], n)
+                    y[q] = y[q + h]
+                else:
+                    O.op(P.op, P.dtype, y[q + h], y[q], n)
+            h *= 2
+    for s, _ in P.segments()[1:]:
+        if P.chain_swap >> s & 1:
+            O.op(P.op, P.dtype, y[0], y[s], n)
+            y[0] = y[s]
+        else:
+            O.op(P.op, P.dtype, y[s], y[0], n)
+    return y[0]
+
+
 def combine_cpu(op, dtype, esize, leaves, folds, shape, n):
     """leaves/folds: lists of uint8 arrays (n*esize bytes) or None."""
     k = len(leaves)
@@ -83,8 +112,7 @@ def run_plans(plans, sends, recvs):
                     assert plans[s].a_send[r].cnt == P.a_recv[s].cnt and plans[s].a_send[r].off == P.a_recv[s].off
         leaves = [sends[P.leaf[q]][lo:hi] for q in range(P.k)]
         folds = [sends[P.leaf_fold[q]][lo:hi] if P.leaf_fold[q] >= 0 else None for q in range(P.k)]
-        out = run_program(P.op, P.dtype, leaves, folds, P.tree_mask, P.chain_mask, P.c_cnt,
-                          P.tree_swap, P.chain_swap)
+        out = run_plan_program(P, leaves, folds, P.c_cnt)
         outs[r] = out
         if not P.c_dst_tmp:
             d = P.c_dst_off * E

@@ -48,7 +48,7 @@ def _worker(rank, world, port, out_dir):
     import mvxtest as T
     import uops
     from oracle import oracle as O
-    from plan_exec import run_program
+    from plan_exec import run_plan_program
 
     mvx = importlib.import_module("mvapich-cce_amd")
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -109,8 +109,7 @@ def _worker(rank, world, port, out_dir):
                 return send[lo:hi] if s == rank else slot[s].numpy()
             leaves = [leaf(P.leaf[q]) for q in range(P.k)]
             folds = [leaf(P.leaf_fold[q]) if P.leaf_fold[q] >= 0 else None for q in range(P.k)]
-            out = run_program(op, dtype, leaves, folds, P.tree_mask, P.chain_mask, P.c_cnt,
-                              P.tree_swap, P.chain_swap)
+            out = run_plan_program(P, leaves, folds, P.c_cnt)
             if not P.c_dst_tmp:
                 recvbuf[P.c_dst_off * E: P.c_dst_off * E + out.size] = out
         # phase C

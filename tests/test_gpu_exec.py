@@ -1,0 +1,193 @@
+"""GPU: the executor around the kernels.
+
+* Host buffers (MPI user buffers live in host memory, allreduce.c:57-92):
+  the staged pipeline slices every rank's plan (mvx_coll.c plan_slice) and
+  overlaps host copies, H2D, the collective and D2H.  Pageable, page-locked
+  and mixed host/device buffers, several slices per call, against the
+  oracle's replay of the reference schedule.
+* Communicators above 8 ranks: combines of more than 8 leaves run as groups
+  of <= 8-leaf launches (predefined ops) or step by step (user ops); p = 9,
+  16, 33 against the replay (binomial Reduce, pairwise / halving
+  Reduce_scatter, Rabenseifner at pof2 = 16 / 32, Scan on ranks >= 8).
+* The reference's argument-test order (mpi_error.h:403-405, 524-526).
+"""
+import numpy as np
+import pytest
+
+import mvxtest as T
+import uops
+
+pytestmark = pytest.mark.gpu
+
+
+def _oracle_coll(oracle, coll, S, R, n_or_cnts, dtype, op, root=0):
+    s8 = [s.view(np.uint8) for s in S]
+    r8 = [r.view(np.uint8) for r in R]
+    if coll == "ar":
+        return oracle.allreduce(s8, r8, n_or_cnts, dtype, op)
+    if coll == "red":
+        return oracle.reduce(s8, r8, n_or_cnts, dtype, op, root)
+    if coll == "scan":
+        return oracle.scan(s8, r8, n_or_cnts, dtype, op)
+    return oracle.reduce_scatter(s8, r8, n_or_cnts, dtype, op)
+
+
+def _call(comm, coll, sends, recvs, n_or_cnts, dtype, op, root=0):
+    if coll == "ar":
+        return comm.allreduce_multi(sends, recvs, n_or_cnts, dtype, op)
+    if coll == "red":
+        return comm.reduce_multi(sends, recvs, n_or_cnts, dtype, op, root)
+    if coll == "scan":
+        return comm.scan_multi(sends, recvs, n_or_cnts, dtype, op)
+    return comm.reduce_scatter_multi(sends, recvs, n_or_cnts, dtype, op)
+
+
+def _pinned_like(a):
+    import torch
+    t = torch.empty(a.nbytes, dtype=torch.uint8, pin_memory=True)
+    t.numpy()[:] = np.ascontiguousarray(a).view(np.uint8)
+    return t
+
+
+def _to_np(buf):
+    import torch
+    if isinstance(buf, torch.Tensor):
+        if buf.is_cuda:
+            torch.cuda.synchronize()
+        return buf.cpu().numpy()
+    return buf
+
+
+@pytest.mark.parametrize("where", ["pageable", "pinned", "send_dev_recv_host", "send_host_recv_dev"])
+@pytest.mark.parametrize("p", [1, 3, 8])
+@pytest.mark.parametrize("coll", ["ar", "red", "rs", "scan"])
+def test_staged_pipeline_matches_reference(mvx, oracle, where, p, coll):
+    import torch
+    comm = mvx.Comm.local_ranks(p, 0)
+    try:
+        for dtype, op in ((10, 102), (17, 111), (8, 105)):
+            E = mvx.dtype_info(dtype)[0]
+            n = (3 << 20) // E + 17          # several 16 MiB slices at p = 8, a ragged tail
+            cnts = [n // p + (r % 3) for r in range(p)] if coll == "rs" else None
+            tot = sum(cnts) if cnts else n
+            S = [T.rand_vec(dtype, tot, 100 * p + r + dtype) for r in range(p)]
+            rb = [(cnts[r] if cnts else n) * E for r in range(p)]
+            if where == "pageable":
+                sends = [T.clone(s).view(np.uint8) for s in S]
+                recvs = [np.zeros(max(b, 1), np.uint8) for b in rb]
+            elif where == "pinned":
+                sends = [_pinned_like(s) for s in S]
+                recvs = [torch.zeros(max(b, 1), dtype=torch.uint8, pin_memory=True) for b in rb]
+            elif where == "send_dev_recv_host":
+                sends = [T.to_dev(s) for s in S]
+                recvs = [np.zeros(max(b, 1), np.uint8) for b in rb]
+            else:
+                sends = [T.clone(s).view(np.uint8) for s in S]
+                recvs = [torch.zeros(max(b, 1), dtype=torch.uint8, device="cuda") for b in rb]
+            root = p - 1
+            r, rcs = _call(comm, coll, sends, recvs, cnts if cnts else n, dtype, op, root)
+            assert r == 0
+            R0 = [np.zeros(max(cnts[q] if cnts else n, 1), S[0].dtype) for q in range(p)]
+            rref = _oracle_coll(oracle, coll, S, R0, cnts if cnts else n, dtype, op, root)
+            assert rcs == rref
+            for q in range(p):
+                if coll == "red" and q != root:
+                    assert not _to_np(recvs[q]).any()    # non-root recvbuf untouched
+                    continue
+                cnt = cnts[q] if cnts else n
+                T.assert_same(op, dtype, _to_np(recvs[q])[: cnt * E], R0[q][:cnt], typemap_only=True)
+    finally:
+        comm.free()
+
+
+WIDE_CASES = [(102, 10), (100, 10), (111, 17), (105, 8), (110, 18)]
+
+
+@pytest.fixture(scope="module")
+def wide(mvx):
+    cs = {p: mvx.Comm.local_ranks(p, 0) for p in (9, 16, 33)}
+    yield cs
+    for c in cs.values():
+        c.free()
+
+
+@pytest.mark.parametrize("p", [9, 16, 33])
+@pytest.mark.parametrize("op,dtype", WIDE_CASES)
+def test_wide_communicators(mvx, oracle, wide, p, op, dtype):
+    import torch
+    comm = wide[p]
+    E = mvx.dtype_info(dtype)[0]
+    for coll, n in (("ar", 7), ("ar", 20000), ("red", 9), ("red", 20000), ("rs", 3), ("rs", 9000), ("scan", 300)):
+        cnts = [n + (r % 2) for r in range(p)] if coll == "rs" else None
+        tot = sum(cnts) if cnts else n
+        S = [T.rand_vec(dtype, tot, 7 * p + r + n) for r in range(p)]
+        ds = [T.to_dev(s) for s in S]
+        drs = [torch.zeros(max((cnts[q] if cnts else n), 1) * E, dtype=torch.uint8, device="cuda")
+               for q in range(p)]
+        root = p // 2
+        r, rcs = _call(comm, coll, ds, drs, cnts if cnts else n, dtype, op, root)
+        assert r == 0
+        R0 = [np.zeros(max(cnts[q] if cnts else n, 1), S[0].dtype) for q in range(p)]
+        rref = _oracle_coll(oracle, coll, S, R0, cnts if cnts else n, dtype, op, root)
+        assert rcs == rref, (coll, n)
+        ranks = [root] if coll == "red" else range(p)
+        for q in ranks:
+            cnt = cnts[q] if cnts else n
+            T.assert_same(op, dtype, T.from_dev(drs[q])[: cnt * E], R0[q][:cnt], typemap_only=True)
+
+
+@pytest.mark.parametrize("device_fn", [False, True], ids=["host_fn", "device_fn"])
+@pytest.mark.parametrize("name,commute", [("mix", 0), ("affine", 0), ("fsum", 1)])
+def test_wide_user_ops(mvx, oracle, wide, name, commute, device_fn):
+    import torch
+    if device_fn:
+        rc, h = mvx.op_create_device(uops.dev_fn(name), commute)
+    else:
+        rc, h = mvx.MPI_Op_create(uops.host_fn(name), commute)
+    assert rc == 0
+    assert oracle.user_op_set(250, uops.host_fn(name), commute) == 0
+    dt = uops.UOPS[name][0]
+    try:
+        for p in (9, 16):
+            comm = wide[p]
+            for coll, n in (("ar", 33), ("red", 33), ("rs", 200), ("scan", 33)):
+                cnts = [n + (r % 2) for r in range(p)] if coll == "rs" else None
+                tot = sum(cnts) if cnts else n
+                S = [uops.rand_for(name, tot, 31 * p + r) for r in range(p)]
+                E = S[0].itemsize
+                ds = [T.to_dev(s) for s in S]
+                drs = [torch.zeros((cnts[q] if cnts else n) * E, dtype=torch.uint8, device="cuda") for q in range(p)]
+                r, rcs = _call(comm, coll, ds, drs, cnts if cnts else n, dt, h, 1)
+                assert r == 0 and rcs == [0] * p
+                R0 = [np.zeros(cnts[q] if cnts else n, S[0].dtype) for q in range(p)]
+                _oracle_coll(oracle, coll, S, R0, cnts if cnts else n, dt, 250, 1)
+                for q in ([1] if coll == "red" else range(p)):
+                    assert T.bytes_equal(T.from_dev(drs[q]), R0[q]), (name, p, coll, q)
+    finally:
+        mvx.MPI_Op_free(h)
+
+
+def test_argument_test_order(mvx):
+    """MPIR_TEST_COUNT and MPIR_TEST_ALIAS both run; each failure advances
+    the error ring, and the later test's code is returned (allreduce.c:76-77
+    count then alias; reduce.c:82-83 and scan.c alias then count).
+    MPI_BOTTOM (NULL) never aliases (mpi_error.h:524-526)."""
+    import torch
+    comm = mvx.Comm.local_ranks(2, 0)
+    x = torch.zeros(16, device="cuda")
+    h = comm.handle
+    assert mvx.MPI_Allreduce(0, 0, 0, 10, 102, h) == 0
+    assert mvx.MPI_Reduce(0, 0, 0, 10, 102, 0, h) == 0
+    assert mvx.MPI_Scan(0, 0, 0, 10, 102, h) == 0
+    a = mvx.MPI_Allreduce(x, x, -1, 10, 102, h)
+    b = mvx.MPI_Allreduce(x, x, -1, 10, 102, h)
+    assert a & 63 == mvx.MPI_ERR_BUFFER and (a >> 6) & 0x7f == 7     # alias wins (tested last)
+    assert (b >> 13) - (a >> 13) == 2                                  # two setmsg calls per call
+    c = mvx.MPI_Reduce(x, x, -1, 10, 102, 0, h)
+    assert c & 63 == mvx.MPI_ERR_COUNT                                 # count tested last
+    assert (c >> 13) - (b >> 13) == 2
+    d = mvx.MPI_Scan(x, x, -1, 10, 102, h)
+    assert d & 63 == mvx.MPI_ERR_COUNT
+    e = mvx.MPI_Reduce_scatter(x, x, [1, 1], 10, 102, h)
+    assert e & 63 == mvx.MPI_ERR_BUFFER and (e >> 13) - (d >> 13) == 1
+    comm.free()
