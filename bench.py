@@ -1,20 +1,30 @@
 #!/usr/bin/env python3
 """Benchmark of the MI355X MPI reduction path (BASELINE.json metric).
 
-  N = 1  config 2: device-resident pairwise MPI_SUM on MPI_FLOAT, 256 MiB
-         vectors -- one step = one local MPI_Op kernel (inout = in + inout).
-  N > 1  config 3 shape: MPI_Allreduce(MPI_SUM, MPI_FLOAT) of 256 MiB per
-         rank, one process per GPU (torchrun), RCCL over xGMI for the
-         exchanges + the reference-order combine kernel.
+  N = 1  config 2 (default): device-resident pairwise MPI_SUM on MPI_FLOAT,
+         256 MiB vectors -- one step = one local MPI_Op kernel
+         (inout = in + inout).
+  N > 1  one process per GPU (torchrun), RCCL over xGMI for the exchanges +
+         the reference-order combine kernel, one step = one collective:
+           c3 (default)  MPI_Allreduce(MPI_SUM, MPI_FLOAT), 256 MiB per rank
+           c4            MPI_Reduce_scatter(MPI_BAND, MPI_LONG), 1 GiB per rank
+           c5            MPI_Allreduce(MPI_MAXLOC, MPI_FLOAT_INT), 64 Mi pairs
 
 value = bytes of input vectors reduced per second over the whole job
-(N x 256 MiB per step / step time), GiB/s.  Inputs are resident in HBM before
-the timed region.  See DESIGN.md section 6 for the roofline accounting.
+(N x bytes per rank per step / step time), GiB/s.  Inputs are resident in HBM
+before the timed region.  Every run checks one untimed step against the
+reference computed on the host by the cpu_baseline leg ("parity"): at N = 1
+the oracle's MPIR_SUM of the same inputs, at N > 1 the reference schedule
+on p host threads (one per rank), which is also the timed cpu_baseline.  The
+exchange variant (mvx_comm_set_exchange) is chosen by time alone (--exchange
+auto); every variant tried reports its parity.  See DESIGN.md sections 5-6.
 """
 import argparse
+import hashlib
 import importlib
 import json
 import os
+import statistics
 import sys
 import time
 
@@ -25,7 +35,15 @@ MIB = 1 << 20
 GIB = 1 << 30
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md, chip-level parameters
 XGMI_LINK_GBS = 153.0           # BASELINE.md section 3 (per link, per direction)
-MPI_SUM, MPI_FLOAT = 102, 10
+MPI_SUM, MPI_FLOAT, MPI_LONG, MPI_FLOAT_INT, MPI_BAND, MPI_MAXLOC = 102, 10, 8, 17, 105, 111
+
+CONFIGS = {
+    # name: (collective, datatype, op, element bytes, default MiB per rank, description)
+    "c3": ("allreduce", MPI_FLOAT, MPI_SUM, 4, 256, "MPI_Allreduce MPI_SUM MPI_FLOAT"),
+    "c4": ("reduce_scatter", MPI_LONG, MPI_BAND, 8, 1024, "MPI_Reduce_scatter MPI_BAND MPI_LONG"),
+    "c5": ("allreduce", MPI_FLOAT_INT, MPI_MAXLOC, 8, 512, "MPI_Allreduce MPI_MAXLOC MPI_FLOAT_INT"),
+}
+EXCH = {"p2p": (0, 0), "pipe": (1, 4), "coll": (2, 0)}
 
 
 def parse():
@@ -33,30 +51,84 @@ def parse():
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--mib", type=int, default=256, help="vector size per rank (MiB)")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--config", default=None, choices=["c2", "c3", "c4", "c5"],
+                    help="c2 at N = 1, c3 at N > 1 by default")
+    ap.add_argument("--mib", type=int, default=0, help="vector MiB per rank (0 = the config's)")
+    ap.add_argument("--no-cpu-baseline", action="store_true",
+                    help="skip the CPU leg (and with it the parity check against it)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r01", "pmc_c2.json"),
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r02", "pmc_c2.json"),
                     help="committed rocprofv3 PMC summary for the traffic field")
     ap.add_argument("--block-cap", type=int, default=0)
     ap.add_argument("--nt-min-log2", type=int, default=0, help="-1 disables non-temporal loads/stores")
     ap.add_argument("--sets", type=int, default=4,
                     help="input sets used round-robin (4 x 512 MiB keeps every step out of the 256 MiB "
                          "Infinity Cache: the number is HBM-bound, not cache-bound)")
+    ap.add_argument("--exchange", default="auto", choices=["auto", "p2p", "pipe", "coll"])
+    ap.add_argument("--tune-steps", type=int, default=5)
+    ap.add_argument("--transport", default="rccl", choices=["rccl", "host"],
+                    help="host: ranks may share a GPU, bytes move through gloo (a test of the "
+                         "multi-GPU leg on a 1-GPU box; not a performance configuration)")
     return ap.parse_args()
 
 
-def synth(n, rank, device):
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _digest(u8):
+    try:
+        import xxhash
+        return xxhash.xxh3_128_hexdigest(memoryview(u8))
+    except ImportError:
+        return hashlib.blake2b(memoryview(u8), digest_size=16).hexdigest()
+
+
+# ---------------------------------------------------------------- inputs ---
+
+def synth_f32(n, seed, device):
     """Mixed-sign f32 with an exponent spread, made on the GPU."""
     import torch
     g = torch.Generator(device=device)
-    g.manual_seed(0x9E3779B9 ^ (rank * 1000003 + 1))
+    g.manual_seed(seed)
     m = torch.randint(-1000000, 1000001, (n,), generator=g, device=device, dtype=torch.int32)
     s = torch.randint(1, 1001, (n,), generator=g, device=device, dtype=torch.int32)
     return (m.to(torch.float32) * 1e-3 * s.to(torch.float32)).contiguous()
 
 
-def cpu_baseline(n_bytes, seconds):
+def synth(cfg, n, rank, device):
+    """Rank `rank`'s send vector of config cfg as a uint8 device tensor: c3
+    mixed-sign f32; c4 int64 words with P(bit = 1) = 15/16 (OR of four random
+    words, so BAND over the ranks is not all zero); c5 {v = u % 1024 (many
+    ties), loc = rank * n + i} FLOAT_INT pairs."""
+    import torch
+    seed = 0x9E3779B9 ^ (rank * 1000003 + 1)
+    if cfg == "c3":
+        return synth_f32(n, seed, device).view(torch.uint8)
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    if cfg == "c4":
+        w = torch.zeros(n, dtype=torch.int64, device=device)
+        for _ in range(4):
+            w |= torch.randint(-(1 << 63), (1 << 63) - 1, (n,), generator=g, device=device, dtype=torch.int64)
+        return w.view(torch.uint8)
+    pair = torch.empty((n, 2), dtype=torch.int32, device=device)
+    pair[:, 0] = torch.randint(0, 1024, (n,), generator=g, device=device, dtype=torch.int32).to(
+        torch.float32).view(torch.int32)
+    pair[:, 1] = torch.arange(n, dtype=torch.int32, device=device) + rank * n
+    return pair.view(-1).view(torch.uint8)
+
+
+# ------------------------------------------------------------------- N = 1 --
+
+def cpu_baseline_op(n_bytes, seconds):
     """Oracle MPIR_SUM (oracle/cpu_ops.c, the reference's loop) on 1 host core."""
     import numpy as np
     from oracle import oracle as O
@@ -79,28 +151,269 @@ def cpu_baseline(n_bytes, seconds):
             "cpu": _cpu_model()}
 
 
-def _cpu_model():
-    try:
-        with open("/proc/cpuinfo") as f:
-            for line in f:
-                if line.startswith("model name"):
-                    return line.split(":", 1)[1].strip()
-    except OSError:
-        pass
-    return "unknown"
+def parity_op(mvx, x_in, x_io, n, stream):
+    """One untimed MPI_SUM step on copies, against the oracle's MPIR_SUM of
+    the same inputs (global_ops.c:364-369) on the host."""
+    import numpy as np
+    import torch
+    from oracle import oracle as O
+    a, b = x_in.clone(), x_io.clone()
+    rc = mvx.op_apply(MPI_SUM, MPI_FLOAT, a, b, n, stream)
+    torch.cuda.synchronize()
+    ref = x_io.cpu().numpy().copy()
+    O.op(MPI_SUM, MPI_FLOAT, x_in.cpu().numpy().view(np.uint8), ref.view(np.uint8), n)
+    ok = rc == 0 and np.array_equal(b.cpu().numpy().view(np.uint32), ref.view(np.uint32))
+    return "bit-exact vs oracle MPIR_SUM (1 step, %d elements)" % n if ok else "MISMATCH (rc=%d)" % rc
 
 
-def load_traffic(path, kernel, nbytes):
-    """Per-launch HBM bytes from a committed rocprofv3 PMC summary, if it was
-    collected for this kernel at this size (FETCH_SIZE doubled on gfx950)."""
+def load_traffic(path, kernel_tag, kernel_symbol, nbytes):
+    """Per-launch HBM bytes from a committed rocprofv3 PMC summary -- only if
+    it was collected for exactly the kernel template this run launched, at
+    this size (FETCH_SIZE doubled on gfx950, tools/pmc_summary.py)."""
     try:
         with open(path) as f:
             d = json.load(f)
     except (OSError, ValueError):
-        return None
-    if d.get("kernel_tag") != kernel or d.get("vector_bytes") != nbytes:
-        return None
-    return d.get("hbm_bytes_per_launch")
+        return None, "no PMC summary at %s" % os.path.relpath(path, ROOT)
+    if d.get("kernel_tag") != kernel_tag or d.get("vector_bytes") != nbytes:
+        return None, "PMC summary is for %s at %s bytes" % (d.get("kernel_tag"), d.get("vector_bytes"))
+    if d.get("kernel_match") != kernel_symbol:
+        return None, "PMC summary template %r != launched %r" % (d.get("kernel_match"), kernel_symbol)
+    return d.get("hbm_bytes_per_launch"), os.path.relpath(path, ROOT)
+
+
+def run_single(args, mvx, dev):
+    import torch
+    nbytes = (args.mib or 256) * MIB
+    n = nbytes // 4
+    stream = torch.cuda.current_stream()
+    x_in = [synth_f32(n, 0x9E3779B9 ^ (2 * s * 1000003 + 1), dev) for s in range(args.sets)]
+    x_io = [synth_f32(n, 0x9E3779B9 ^ ((2 * s + 1) * 1000003 + 1), dev) for s in range(args.sets)]
+    # cpu_baseline leg, part 1: the reference op on the same inputs (checker)
+    parity = None if args.no_cpu_baseline else parity_op(mvx, x_in[0], x_io[0], n, stream)
+    it = [0]
+
+    def step():
+        s = it[0] % args.sets
+        it[0] += 1
+        rc = mvx.op_apply(MPI_SUM, MPI_FLOAT, x_in[s], x_io[s], n, stream)
+        if rc:
+            raise RuntimeError("mvx_op_apply rc=%d" % rc)
+
+    times = timed(args, step, stream, 1)
+    kernel = mvx.last_kernel()
+    symbol = mvx.last_kernel_symbol()
+    kern_s = times["dev_ms"] / 1e3 / args.steps           # HIP events on the launch stream
+    alg_bytes = 3 * nbytes                                  # read in, read inout, write inout
+    achieved = alg_bytes / kern_s / 1e9
+    traffic, tsrc = load_traffic(args.pmc, kernel, symbol, nbytes)
+    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": tsrc,
+            "kernel": kernel, "kernel_symbol": symbol, "kernel_us": round(kern_s * 1e6, 2),
+            "kernel_us_median": round(times["median_ms"] * 1e3, 2), "kernel_us_min": round(times["min_ms"] * 1e3, 2),
+            "alg_bytes_per_launch": alg_bytes}
+    out = result(args, 1, nbytes, times, "f32",
+                 {"workload": "config2: device-resident pairwise MPI_SUM float32 %d MiB (local MPI_Op kernel), "
+                              "%d input sets round-robin" % (nbytes // MIB, args.sets),
+                  "vector_bytes_per_rank": nbytes, "op": "MPI_SUM", "datatype": "MPI_FLOAT",
+                  "parallelism": "single GPU"}, roof)
+    out["parity"] = parity
+    if not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline_op(nbytes, args.cpu_seconds)
+    print(json.dumps(out), flush=True)
+
+
+# ------------------------------------------------------------------ common --
+
+def timed(args, step, stream, world):
+    """W untimed steps, then K steps between barrier + synchronize; per-step
+    HIP events on the launch stream give mean / median / min."""
+    import torch
+    import torch.distributed as dist
+
+    def barrier():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+    t0 = time.perf_counter()
+    evs[0].record(stream)
+    for i in range(args.steps):
+        step()
+        evs[i + 1].record(stream)
+    barrier()
+    wall = time.perf_counter() - t0
+    per = [evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)]
+    dev_ms = evs[0].elapsed_time(evs[-1])
+    t_local = max(wall, dev_ms / 1e3)
+    if world > 1:
+        t = torch.tensor([t_local], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        t_local = float(t.item())
+    return {"t_job": t_local, "dev_ms": dev_ms, "mean_ms": dev_ms / args.steps,
+            "median_ms": statistics.median(per), "min_ms": min(per)}
+
+
+def result(args, world, nbytes, times, dtype, config, roof):
+    ms_per_step = times["t_job"] * 1e3 / args.steps
+    return {
+        "metric": "GiB/s device-resident Allreduce(SUM,float32) at 1/2/4/8 GPUs; % HBM/xGMI peak",
+        "value": round(world * nbytes * args.steps / times["t_job"] / GIB, 2), "unit": "GiB/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 5),
+        "step_ms": {"mean": round(times["mean_ms"], 5), "median": round(times["median_ms"], 5),
+                    "min": round(times["min_ms"], 5)},
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": dtype,
+        "data": "synthetic (generated on device, SURVEY.md 8(d) distributions)",
+        "config": config, "roofline": roof,
+    }
+
+
+# ------------------------------------------------------------------- N > 1 --
+
+def reference_run(cfg, world, n, dev, want_time):
+    """Rank 0: every rank's inputs (same generator), the reference schedule
+    on `world` host threads (oracle/cpu_coll.c, one thread per rank, as the
+    reference's p processes) -> per-rank result digests and seconds per
+    collective."""
+    import numpy as np
+    import torch
+    from oracle import oracle as O
+    coll, dtype, op, E, _, _ = CONFIGS[cfg]
+    sends = []
+    for r in range(world):
+        sends.append(synth(cfg, n, r, dev).cpu().numpy())
+        torch.cuda.empty_cache()
+    cnts = [n // world] * world if coll == "reduce_scatter" else None
+    nrecv = (n // world) if cnts else n
+    recvs = [np.zeros(nrecv * E, np.uint8) for _ in range(world)]
+    ocoll = 3 if cnts else 1
+    # scratch per rank thread: the whole vector (Allreduce), the rank's block
+    # (pairwise Reduce_scatter), or 2 x the vector (recursive halving)
+    tmp_elems = n if not cnts else (nrecv if O.algorithm(ocoll, world, n, dtype) == O.ALG_RS_PAIRWISE else 2 * n)
+    tmps = [np.zeros(tmp_elems * E, np.uint8) for _ in range(world)]
+    secs = O.threads_coll(ocoll, sends, recvs, tmps, n, dtype, op, 0, cnts, 1)
+    digests = [_digest(r) for r in recvs]
+    reps = 0
+    if want_time:
+        reps = max(1, min(20, int(10.0 / max(secs, 1e-3))))
+        secs = O.threads_coll(ocoll, sends, recvs, tmps, n, dtype, op, 0, cnts, reps)
+    del sends, tmps
+    return digests, secs, reps
+
+
+def run_multi(args, mvx, dev, world, rank, local):
+    import torch
+    import torch.distributed as dist
+    cfg = args.config or "c3"
+    coll, dtype, op, E, mib, desc = CONFIGS[cfg]
+    nbytes = (args.mib or mib) * MIB
+    n = nbytes // E
+    n -= n % world
+    nbytes = n * E
+    stream = torch.cuda.current_stream()
+    if args.transport == "host":
+        tp = importlib.import_module("mvapich-cce_amd.transport")
+        comm = mvx.Comm.from_transport(tp.TorchP2PTransport(), dev.index)
+    else:
+        comm = mvx.Comm.from_torch_distributed(dev.index)
+    sets = max(1, min(args.sets, 2))
+    sendbuf = [synth(cfg, n, rank, dev) for _ in range(sets)]
+    nrecv = n // world if coll == "reduce_scatter" else n
+    recvbuf = [torch.empty(nrecv * E, dtype=torch.uint8, device=dev) for _ in range(sets)]
+    cnts = [n // world] * world
+    comm.reserve(2 * nbytes)
+    it = [0]
+
+    def step():
+        s = it[0] % sets
+        it[0] += 1
+        if coll == "allreduce":
+            rc = comm.allreduce_async(sendbuf[s], recvbuf[s], n, dtype, op, stream)
+        else:
+            rc = comm.reduce_scatter_async(sendbuf[s], recvbuf[s], cnts, dtype, op, stream)
+        if rc:
+            raise RuntimeError("%s rc=%d" % (coll, rc))
+
+    # the reference's result (and the CPU baseline) on rank 0's host
+    # cpu_baseline leg: the reference schedule on p host threads -- timed, and
+    # its per-rank results are the parity reference
+    ref, cpu = None, None
+    if not args.no_cpu_baseline:
+        if rank == 0:
+            ref, secs, reps = reference_run(cfg, world, n, dev, True)
+            cpu = {"value": round(world * nbytes / secs / GIB, 3), "unit": "GiB/s", "cores": world,
+                   "kind": "port",
+                   "sample": "reference schedule (oracle/cpu_coll.c) of the same %s on %d host threads, "
+                             "one per rank, %d reps" % (cfg, world, reps),
+                   "cpu": _cpu_model(), "ms_per_collective": round(secs * 1e3, 3)}
+        box = [ref]
+        dist.broadcast_object_list(box, src=0)
+        ref = box[0]
+
+    def check():
+        """one untimed step on set 0, every rank's digest against rank 0's reference"""
+        it[0] = 0
+        step()
+        torch.cuda.synchronize()
+        mine = _digest(recvbuf[0].cpu().numpy())
+        allg = [None] * world
+        dist.all_gather_object(allg, mine)
+        return allg == ref
+
+    # exchange variants: timed, the fastest chosen on rank 0; each reports
+    # its parity against the reference
+    names = ["p2p", "pipe", "coll"] if args.exchange == "auto" else [args.exchange]
+    tried = {}
+    for name in names:
+        mode, slices = EXCH[name]
+        comm.set_exchange(mode, slices)
+        ok = check() if ref is not None else None
+        t = torch.zeros(1, dtype=torch.float64)
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.tune_steps):
+            step()
+        torch.cuda.synchronize()
+        t[0] = time.perf_counter() - t0
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        tried[name] = {"ms_per_step": round(float(t.item()) * 1e3 / args.tune_steps, 4), "parity": ok}
+    choice = min(names, key=lambda k: tried[k]["ms_per_step"])
+    box = [choice]
+    dist.broadcast_object_list(box, src=0)
+    choice = box[0]
+    comm.set_exchange(*EXCH[choice])
+    parity = tried[choice]["parity"]
+
+    times = timed(args, step, stream, world)
+    p = world
+    sec = times["t_job"] / args.steps
+    if coll == "allreduce":
+        busbw = 2 * (p - 1) / p * nbytes / sec / 1e9
+        note = "busbw = 2(p-1)/p*S/t"
+    else:
+        busbw = (p - 1) / p * nbytes / sec / 1e9
+        note = "busbw = (p-1)/p*S/t"
+    links = min(p - 1, 7)
+    peak = links * XGMI_LINK_GBS
+    roof = {"bound": "xgmi", "achieved": round(busbw, 1), "peak": peak, "unit": "GB/s",
+            "frac": round(busbw / peak, 4), "traffic": None, "kernel": mvx.last_kernel(),
+            "note": "%s against %d direct xGMI links x %.0f GB/s" % (note, links, XGMI_LINK_GBS),
+            "combine_hbm_bytes_per_step": (p + 1) * nbytes // p}
+    out = result(args, world, nbytes, times, {"c3": "f32", "c4": "int64", "c5": "f32+int32"}[cfg],
+                 {"workload": "%s: %s %d MiB per rank, RCCL xGMI exchange + reference-order combine"
+                              % (cfg, desc, nbytes // MIB),
+                  "vector_bytes_per_rank": nbytes, "parallelism": "dp%d (blocks sharded over ranks)" % p,
+                  "exchange": choice, "exchange_tuning": tried, "transport": args.transport}, roof)
+    out["parity"] = (("bit-exact vs the reference schedule, all %d ranks" % p) if parity
+                     else ("MISMATCH" if parity is False else None))
+    out["cpu_baseline"] = cpu
+    comm.free()
+    return out
 
 
 def main():
@@ -111,116 +424,24 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("gloo", rank=rank, world_size=world)
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    dev_index = local % torch.cuda.device_count() if args.transport == "host" else local
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
     mvx = importlib.import_module("mvapich-cce_amd")
     if args.block_cap or args.nt_min_log2:
         mvx.set_launch(args.block_cap, args.nt_min_log2)
-
-    nbytes = args.mib * MIB
-    n = nbytes // 4
-    stream = torch.cuda.current_stream()
-
-    def barrier():
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-
-    it = [0]
     if world == 1:
-        x_in = [synth(n, 2 * s, dev) for s in range(args.sets)]
-        x_io = [synth(n, 2 * s + 1, dev) for s in range(args.sets)]
-
-        def step():
-            s = it[0] % args.sets
-            it[0] += 1
-            rc = mvx.op_apply(MPI_SUM, MPI_FLOAT, x_in[s], x_io[s], n, stream)
-            if rc:
-                raise RuntimeError("mvx_op_apply rc=%d" % rc)
-        comm = None
-    else:
-        comm = mvx.Comm.from_torch_distributed(local)
-        sets = max(1, min(args.sets, 2))
-        sendbuf = [synth(n, rank * 16 + s, dev) for s in range(sets)]
-        recvbuf = [torch.empty_like(sendbuf[0]) for _ in range(sets)]
-        comm.reserve(2 * nbytes)
-
-        def step():
-            s = it[0] % sets
-            it[0] += 1
-            rc = comm.allreduce_async(sendbuf[s], recvbuf[s], n, MPI_FLOAT, MPI_SUM, stream)
-            if rc:
-                raise RuntimeError("mvx_allreduce_async rc=%d" % rc)
-
-    for _ in range(args.warmup):
-        step()
-    barrier()
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for _ in range(args.steps):
-        step()
-    ev1.record(stream)
-    barrier()
-    wall = time.perf_counter() - t0
-    dev_ms = ev0.elapsed_time(ev1)
-    t_local = max(wall, dev_ms / 1e3)
-    if world > 1:
-        t = torch.tensor([t_local], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        t_job = float(t.item())
-    else:
-        t_job = t_local
-    kernel = mvx.last_kernel()
-    ms_per_step = t_job * 1e3 / args.steps
-    value = world * nbytes * args.steps / t_job / GIB
-
-    if world == 1:
-        kern_s = dev_ms / 1e3 / args.steps           # HIP events on the launch stream
-        alg_bytes = 3 * nbytes                         # read in, read inout, write inout
-        achieved = alg_bytes / kern_s / 1e9
-        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": load_traffic(args.pmc, kernel, nbytes),
-                "kernel": kernel, "kernel_us": round(kern_s * 1e6, 2), "alg_bytes_per_launch": alg_bytes}
-        workload = ("config2: device-resident pairwise MPI_SUM float32 %d MiB (local MPI_Op kernel), "
-                    "%d input sets round-robin" % (args.mib, args.sets))
-        par = "single GPU"
-    else:
-        p = world
-        busbw = 2 * (p - 1) / p * nbytes / (ms_per_step / 1e3) / 1e9
-        links = min(p - 1, 7)
-        peak = links * XGMI_LINK_GBS
-        roof = {"bound": "xgmi", "achieved": round(busbw, 1), "peak": peak, "unit": "GB/s",
-                "frac": round(busbw / peak, 4), "traffic": None, "kernel": kernel,
-                "note": "busbw = 2(p-1)/p*S/t against %d direct xGMI links" % links}
-        workload = "config3-shape: MPI_Allreduce SUM float32 %d MiB per rank, RCCL xGMI exchange + combine" % args.mib
-        par = "dp%d (blocks sharded over ranks)" % p
-
-    out = {
-        "metric": "GiB/s device-resident Allreduce(SUM,float32) at 1/2/4/8 GPUs; % HBM/xGMI peak",
-        "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": round(ms_per_step, 5), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-        "data": "synthetic (mixed-sign f32, generated on device)",
-        "config": {"workload": workload, "vector_bytes_per_rank": nbytes, "op": "MPI_SUM",
-                   "datatype": "MPI_FLOAT", "parallelism": par},
-        "roofline": roof,
-    }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(nbytes, args.cpu_seconds)
-    elif rank == 0:
-        out["cpu_baseline"] = None
-    if comm is not None:
-        comm.free()
+        if args.config not in (None, "c2"):
+            sys.exit("configs c3-c5 are multi-GPU: run under torchrun with --nproc-per-node N")
+        run_single(args, mvx, dev)
+        return
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    out = run_multi(args, mvx, dev, world, rank, local)
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
+    dist.barrier()
+    dist.destroy_process_group()
 
 
 if __name__ == "__main__":

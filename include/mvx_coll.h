@@ -40,6 +40,27 @@ int mvx_comm_init(MPI_Comm *comm, int rank, int size, int device,
 /* `size` virtual ranks in this process on one device (loopback transport,
  * device-to-device copies); use the *_multi entry points with it. */
 int mvx_comm_init_local(MPI_Comm *comm, int size, int device);
+
+/* One process per rank with a caller-supplied transport instead of RCCL
+ * (e.g. several processes sharing one GPU, bytes moved by a host library).
+ * A phase is start, then send / recv calls (device buffers, enqueued work on
+ * `stream` must complete before the bytes are read), then end, which
+ * performs them and returns once the received bytes are in place and
+ * visible to later work on `stream`.  Sends and receives between one pair
+ * of ranks pair up in call order.  Callbacks return 0 or an error. */
+typedef struct mvx_transport {
+    void *ctx;
+    int (*start)(void *ctx);
+    int (*send)(void *ctx, const void *buf, size_t bytes, int peer, void *stream);
+    int (*recv)(void *ctx, void *buf, size_t bytes, int peer, void *stream);
+    int (*end)(void *ctx, void *stream);
+} mvx_transport;
+int mvx_comm_init_transport(MPI_Comm *comm, int rank, int size, int device,
+                            const mvx_transport *transport);
+/* helpers for transports: a blocking copy between any two pointers
+ * (hipMemcpyDefault) and a stream synchronisation */
+int mvx_copy(void *dst, const void *src, size_t bytes);
+int mvx_stream_synchronize(void *stream);
 int mvx_comm_free(MPI_Comm *comm);
 int MPI_Comm_size(MPI_Comm comm, int *size);
 int MPI_Comm_rank(MPI_Comm comm, int *rank);
@@ -47,6 +68,22 @@ int MPI_Comm_rank(MPI_Comm comm, int *rank);
 int mvx_comm_set_stream(MPI_Comm comm, void *hip_stream);
 /* pre-size the staging pool so no allocation happens inside a call */
 int mvx_comm_reserve(MPI_Comm comm, size_t bytes);
+
+/* How a communicator moves blocks between ranks (device buffers).  All
+ * variants compute the same bits; they differ in how xGMI is driven.
+ *   MVX_EXCH_P2P   phases as grouped ncclSend / ncclRecv (default)
+ *   MVX_EXCH_PIPE  the plan in `slices` slices: the exchange of slice t and
+ *                  the distribution of slice t-2 share one transfer group
+ *                  while slice t-1 is combined on a second stream
+ *   MVX_EXCH_COLL  ncclAllToAll + in-place ncclAllGather when every rank
+ *                  holds p equal blocks (Allreduce / Reduce_scatter with
+ *                  count % p == 0, p a power of two); P2P otherwise
+ * Env at creation: MVX_EXCHANGE = p2p | pipe[:slices] | coll. */
+#define MVX_EXCH_P2P  0
+#define MVX_EXCH_PIPE 1
+#define MVX_EXCH_COLL 2
+int mvx_comm_set_exchange(MPI_Comm comm, int mode, int slices);
+int mvx_comm_get_exchange(MPI_Comm comm, int *mode, int *slices);
 
 /* ---- MPI API (blocking) ------------------------------------------------ */
 int MPI_Reduce(void *sendbuf, void *recvbuf, int count, MPI_Datatype datatype,

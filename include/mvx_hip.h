@@ -107,8 +107,11 @@ unsigned mvx_chain_mask(int k);
  * MVX_NT_MIN_BYTES.  Defaults: one-pass grid, non-temporal from 64 MiB. */
 void mvx_hip_set_launch(int block_cap, int nt_min_bytes_log2);
 
-/* Name of the last kernel launched (for profile attribution in bench.py). */
+/* Name of the last kernel launched (for profile attribution in bench.py):
+ * a short tag ("sum_f32_k2_nt"), and the template as rocprofv3 reports it
+ * ("k_combine<2, float, 2, 4, 1>"). */
 const char *mvx_hip_last_kernel(void);
+const char *mvx_hip_last_kernel_symbol(void);
 
 #ifdef __cplusplus
 }

@@ -119,13 +119,19 @@ def _load():
     _hip.mvx_hip_set_launch.argtypes = [i, i]
     _hip.mvx_hip_set_launch.restype = None
     _hip.mvx_hip_last_kernel.restype = ctypes.c_char_p
+    _hip.mvx_hip_last_kernel_symbol.restype = ctypes.c_char_p
     c = _coll
     c.mvx_get_unique_id.argtypes = [vp]
     c.mvx_comm_init.argtypes = [pi, i, i, i, vp]
     c.mvx_comm_init_local.argtypes = [pi, i, i]
+    c.mvx_comm_init_transport.argtypes = [pi, i, i, i, vp]
+    c.mvx_copy.argtypes = [vp, vp, sz]
+    c.mvx_stream_synchronize.argtypes = [vp]
     c.mvx_comm_free.argtypes = [pi]
     c.mvx_comm_set_stream.argtypes = [i, vp]
     c.mvx_comm_reserve.argtypes = [i, sz]
+    c.mvx_comm_set_exchange.argtypes = [i, i, i]
+    c.mvx_comm_get_exchange.argtypes = [i, pi, pi]
     c.MPI_Comm_size.argtypes = [i, pi]
     c.MPI_Comm_rank.argtypes = [i, pi]
     c.mvx_buffer_is_device.argtypes = [vp]

@@ -12,7 +12,7 @@ from .consts import COLL_ALLREDUCE, COLL_REDUCE, COLL_REDUCE_SCATTER  # noqa: F4
 __all__ = [
     "addr", "stream_handle", "op_apply", "op_combine", "op_program", "Comm",
     "MPI_Allreduce", "MPI_Reduce", "MPI_Reduce_scatter", "MPI_Scan", "MPI_Op_create", "MPI_Op_free", "op_create_device",
-    "MPIR_call", "op_errno", "last_kernel", "set_launch",
+    "MPIR_call", "op_errno", "last_kernel", "last_kernel_symbol", "set_launch",
     "MPI_Type_contiguous", "MPI_Type_commit", "MPI_Type_free", "MPI_Type_extent", "MPI_Type_size",
 ]
 
@@ -74,6 +74,11 @@ def last_kernel():
     return hip().mvx_hip_last_kernel().decode()
 
 
+def last_kernel_symbol():
+    """The last launched kernel template, as rocprofv3 names it."""
+    return hip().mvx_hip_last_kernel_symbol().decode()
+
+
 # ------------------------------------------------------------- communicators
 
 class Comm:
@@ -106,6 +111,24 @@ class Comm:
         return cls(h.value, rank, size, False)
 
     @classmethod
+    def from_transport(cls, transport, device=None):
+        """One rank per process with a host transport (mvx_comm_init_transport),
+        e.g. transport.TorchP2PTransport over an initialised gloo group; several
+        processes may share one GPU."""
+        import torch
+        import torch.distributed as dist
+        rank, size = dist.get_rank(), dist.get_world_size()
+        if device is None:
+            device = torch.cuda.current_device()
+        h = ctypes.c_int()
+        rc = coll().mvx_comm_init_transport(ctypes.byref(h), rank, size, device, ctypes.byref(transport.struct()))
+        if rc:
+            raise RuntimeError("mvx_comm_init_transport rc=%d" % rc)
+        c = cls(h.value, rank, size, False)
+        c.transport = transport      # keeps the callbacks alive
+        return c
+
+    @classmethod
     def local_ranks(cls, size, device=0):
         """`size` virtual ranks on one device (use the *_multi methods)."""
         h = ctypes.c_int()
@@ -123,6 +146,17 @@ class Comm:
 
     def reserve(self, nbytes):
         return coll().mvx_comm_reserve(self.handle, nbytes)
+
+    def set_exchange(self, mode, slices=0):
+        """EXCH_P2P / EXCH_PIPE (with `slices`) / EXCH_COLL (mvx_comm_set_exchange)."""
+        return coll().mvx_comm_set_exchange(self.handle, mode, slices)
+
+    def get_exchange(self):
+        m, s = ctypes.c_int(), ctypes.c_int()
+        rc = coll().mvx_comm_get_exchange(self.handle, ctypes.byref(m), ctypes.byref(s))
+        if rc:
+            raise RuntimeError("mvx_comm_get_exchange rc=%d" % rc)
+        return m.value, s.value
 
     def get_tuning(self):
         """The communicator's device flavour and knobs (a Tuning)."""

@@ -70,6 +70,11 @@ typedef struct {
     size_t uhost_bytes;
     mvx_tuning tune;     /* device flavour + knobs (mvx_coll.h) */
     int shmem_block;     /* claimed shmem collective block, -1 = none */
+    int exch, exch_slices;      /* exchange variant, MVX_EXCH_* (mvx_coll.h) */
+    int has_ops;                /* caller-supplied transport instead of RCCL */
+    mvx_transport ops;
+    hipStream_t cstream;        /* combine stream of the pipelined exchange */
+    hipEvent_t pev[4];          /* its exchange-done / combine-done events */
 } mvx_comm_t;
 
 static mvx_comm_t g_comms[MAX_COMMS];
@@ -162,6 +167,21 @@ static int claim_shmem_block(void)
     return -1;
 }
 
+/* MVX_EXCHANGE = p2p | pipe[:slices] | coll (default p2p) */
+static void exchange_from_env(mvx_comm_t *c)
+{
+    const char *e = getenv("MVX_EXCHANGE");
+    c->exch = MVX_EXCH_P2P;
+    c->exch_slices = 4;
+    if (!e) return;
+    if (!strncmp(e, "pipe", 4)) {
+        c->exch = MVX_EXCH_PIPE;
+        if (e[4] == ':' && atoi(e + 5) > 0) c->exch_slices = atoi(e + 5);
+    } else if (!strcmp(e, "coll")) {
+        c->exch = MVX_EXCH_COLL;
+    }
+}
+
 /* a new communicator's flavour: MVX_DEVICE names the reference device */
 static int comm_flavour(mvx_comm_t *c)
 {
@@ -169,6 +189,7 @@ static int comm_flavour(mvx_comm_t *c)
     const int smp = d && (!strcmp(d, "ch_gen2") || !strcmp(d, "ch_smp") || !strcmp(d, "ch_gen2_ud"));
     int rc = mvx_tuning_from_env(&c->tune, smp);
     c->shmem_block = -1;
+    exchange_from_env(c);
     if (rc) return rc;
     if (c->tune.smp && c->tune.enable_shmem_collectives) {
         c->shmem_block = claim_shmem_block();
@@ -226,6 +247,34 @@ int mvx_comm_init_local(MPI_Comm *comm, int size, int device)
     return MPI_SUCCESS;
 }
 
+int mvx_comm_init_transport(MPI_Comm *comm, int rank, int size, int device,
+                            const mvx_transport *transport)
+{
+    mvx_comm_t *c;
+    if (!comm || !transport || !transport->start || !transport->send || !transport->recv ||
+        !transport->end || size < 1 || size > MVX_MAXP || rank < 0 || rank >= size)
+        return MPI_ERR_ARG;
+    if (hipSetDevice(device) != hipSuccess) return MPI_ERR_OTHER;
+    c = new_comm(comm);
+    if (!c) return MPI_ERR_INTERN;
+    c->rank = rank; c->size = size; c->device = device; c->local = 0;
+    if (comm_flavour(c)) { c->used = 0; return MPI_ERR_OTHER; }
+    c->has_ops = 1;
+    c->ops = *transport;
+    publish_comm(c, comm);
+    return MPI_SUCCESS;
+}
+
+int mvx_copy(void *dst, const void *src, size_t bytes)
+{
+    return hipMemcpy(dst, src, bytes, hipMemcpyDefault) == hipSuccess ? MPI_SUCCESS : MPI_ERR_OTHER;
+}
+
+int mvx_stream_synchronize(void *stream)
+{
+    return hipStreamSynchronize((hipStream_t)stream) == hipSuccess ? MPI_SUCCESS : MPI_ERR_OTHER;
+}
+
 int mvx_comm_free(MPI_Comm *comm)
 {
     mvx_comm_t *c = comm ? get_comm(*comm) : NULL;
@@ -235,6 +284,11 @@ int mvx_comm_free(MPI_Comm *comm)
     if (c->hpool) hipFree(c->hpool);
     if (c->upool) hipFree(c->upool);
     if (c->uhost) hipHostFree(c->uhost);
+    if (c->cstream) {
+        int i;
+        hipStreamDestroy(c->cstream);
+        for (i = 0; i < 4; i++) hipEventDestroy(c->pev[i]);
+    }
     release_shmem_block(c);
     if (c->handle == MPI_COMM_WORLD) g_have_world = 0;
     memset(c, 0, sizeof *c);
@@ -275,6 +329,25 @@ int mvx_comm_set_tuning(MPI_Comm comm, const mvx_tuning *t)
     if (!c) return ERR_COMM_NULL_CODE;
     if (!t) return MPI_ERR_ARG;
     c->tune = *t;
+    return MPI_SUCCESS;
+}
+
+int mvx_comm_set_exchange(MPI_Comm comm, int mode, int slices)
+{
+    mvx_comm_t *c = get_comm(comm);
+    if (!c) return ERR_COMM_NULL_CODE;
+    if (mode < MVX_EXCH_P2P || mode > MVX_EXCH_COLL || slices < 0) return MPI_ERR_ARG;
+    c->exch = mode;
+    if (slices > 0) c->exch_slices = slices;
+    return MPI_SUCCESS;
+}
+
+int mvx_comm_get_exchange(MPI_Comm comm, int *mode, int *slices)
+{
+    mvx_comm_t *c = get_comm(comm);
+    if (!c) return ERR_COMM_NULL_CODE;
+    if (mode) *mode = c->exch;
+    if (slices) *slices = c->exch_slices;
     return MPI_SUCCESS;
 }
 
@@ -497,7 +570,7 @@ static int combine_user(mvx_comm_t *c, const mvx_plan *P, const void *const *src
     const size_t bytes = (size_t)(n * E), slot = (bytes + 255) & ~(size_t)255;
     const int dev = o && o->dop;
     const hipMemcpyKind in_kind = dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
-    char *y[MVX_MAXK], *base;
+    char *y[MVX_MAXK] = {0}, *base;
     int q, l, s, e, rc;
     if (!o) return MPI_ERR_OP;
     if (dev) rc = grow(&c->upool, &c->upool_bytes, slot * (size_t)P->k * 2);
@@ -660,6 +733,9 @@ typedef struct mvx_xport {
     int (*recv)(struct mvx_xport *, void *, size_t, int, hipStream_t);
     ncclComm_t nccl;
     loopback_t *lb;
+    const mvx_transport *ops;   /* caller-supplied transport */
+    hipStream_t st;             /* the stream its phases end on */
+    int depth;                  /* nesting of start / end (one group) */
     int me;
 } mvx_xport;
 
@@ -669,6 +745,22 @@ static int nc_send(mvx_xport *t, const void *b, size_t n, int peer, hipStream_t 
 { return ncclSend(b, n, ncclUint8, peer, t->nccl, st) == ncclSuccess ? 0 : MPI_ERR_OTHER; }
 static int nc_recv(mvx_xport *t, void *b, size_t n, int peer, hipStream_t st)
 { return ncclRecv(b, n, ncclUint8, peer, t->nccl, st) == ncclSuccess ? 0 : MPI_ERR_OTHER; }
+
+/* a caller-supplied transport; nested start / end pairs form one group */
+static int op_start(mvx_xport *t)
+{
+    if (t->depth++) return 0;
+    return t->ops->start(t->ops->ctx) ? MPI_ERR_OTHER : 0;
+}
+static int op_end(mvx_xport *t)
+{
+    if (--t->depth) return 0;
+    return t->ops->end(t->ops->ctx, (void *)t->st) ? MPI_ERR_OTHER : 0;
+}
+static int op_send(mvx_xport *t, const void *b, size_t n, int peer, hipStream_t st)
+{ return t->ops->send(t->ops->ctx, b, n, peer, (void *)st) ? MPI_ERR_OTHER : 0; }
+static int op_recv(mvx_xport *t, void *b, size_t n, int peer, hipStream_t st)
+{ return t->ops->recv(t->ops->ctx, b, n, peer, (void *)st) ? MPI_ERR_OTHER : 0; }
 
 static int lb_nop(mvx_xport *t) { (void)t; return 0; }
 static int lb_send(mvx_xport *t, const void *b, size_t n, int peer, hipStream_t st)
@@ -922,23 +1014,51 @@ typedef struct {
     mvx_xport *t;                    /* nr transports */
 } job_t;
 
-static int job_layout(mvx_comm_t *c, rank_exec_t *X, const job_t *J, const mvx_plan *Q)
+static size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+/* every local rank's staging region for plans Q: X[r].P / c set, per-rank
+ * offsets in off[], total bytes returned (pool not touched) */
+static size_t region_layout(mvx_comm_t *c, rank_exec_t *X, const job_t *J, const mvx_plan *Q, size_t *off)
 {
-    size_t need = 0, base[MVX_MAXP];
-    int r, rc;
+    size_t need = 0;
+    int r;
     for (r = 0; r < J->nr; r++) {
         X[r].P = &Q[r];
         X[r].c = c;
-        base[r] = (need + 255) & ~(size_t)255;
-        need = base[r] + exec_layout(&X[r]);
+        off[r] = (need + 255) & ~(size_t)255;
+        need = off[r] + exec_layout(&X[r]);
     }
+    return (need + 255) & ~(size_t)255;
+}
+
+static int job_layout(mvx_comm_t *c, rank_exec_t *X, const job_t *J, const mvx_plan *Q)
+{
+    size_t off[MVX_MAXP];
+    const size_t need = region_layout(c, X, J, Q, off);
+    int r, rc;
     if ((rc = grow(&c->pool, &c->pool_bytes, need))) return rc;
-    for (r = 0; r < J->nr; r++) X[r].pool = c->pool + base[r];
+    for (r = 0; r < J->nr; r++) X[r].pool = c->pool + off[r];
     return MPI_SUCCESS;
 }
 
-/* all buffers in HBM: the whole plan at once */
-static int run_device(mvx_comm_t *c, const job_t *J, hipStream_t st)
+/* ---- exchange variants (MVX_EXCH_*) -------------------------------------
+ * PIPE: the plan runs in slices; slice t's exchange and slice t-2's
+ * distribution go in one transfer group while slice t-1 is combined on a
+ * second stream, so xGMI and HBM work at once.  Slices keep every block
+ * boundary (plan_slice), so the bits are the unsliced plan's. */
+static mvx_plan g_pipe[3][MVX_MAXP];
+
+static int pipe_streams(mvx_comm_t *c)
+{
+    int i;
+    if (c->cstream) return MPI_SUCCESS;
+    if (hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking) != hipSuccess) return MPI_ERR_OTHER;
+    for (i = 0; i < 4; i++)
+        if (hipEventCreateWithFlags(&c->pev[i], hipEventDisableTiming) != hipSuccess) return MPI_ERR_OTHER;
+    return MPI_SUCCESS;
+}
+
+static int run_device_plain(mvx_comm_t *c, const job_t *J, hipStream_t st)
 {
     rank_exec_t X[MVX_MAXP];
     int r, rc;
@@ -948,6 +1068,123 @@ static int run_device(mvx_comm_t *c, const job_t *J, hipStream_t st)
     }
     if ((rc = job_layout(c, X, J, J->P))) return rc;
     return exec_group(X, J->t, J->nr, st);
+}
+
+static int run_device_pipe(mvx_comm_t *c, const job_t *J, hipStream_t st)
+{
+    static rank_exec_t X0[MVX_MAXP], X[3][MVX_MAXP];
+    size_t off[MVX_MAXP], region;
+    long span = 0, cs, nsl, t;
+    int r, rc, q;
+    const int ns = c->exch_slices > 0 ? c->exch_slices : 4;
+    for (r = 0; r < J->nr; r++)
+        if (plan_span(&J->P[r]) > span) span = plan_span(&J->P[r]);
+    cs = (span + ns - 1) / ns;
+    cs = (cs + 255) & ~255L;
+    nsl = (span + cs - 1) / cs;
+    if (nsl <= 1) return run_device_plain(c, J, st);
+    if ((rc = pipe_streams(c))) return rc;
+    for (r = 0; r < J->nr; r++) {
+        plan_slice(&J->P[r], 0, cs, &g_pipe[0][r]);
+        X0[r].sendbuf = J->send[r];
+        X0[r].recvbuf = J->recv[r];
+    }
+    region = region_layout(c, X0, J, g_pipe[0], off);   /* slice 0 is the largest */
+    if ((rc = grow(&c->pool, &c->pool_bytes, 2 * region))) return rc;
+    for (t = 0; t < nsl + 2; t++) {
+        const int a = t < nsl, dist = t >= 2;
+        const int cur = (int)(t % 3), old = (int)((t + 1) % 3);   /* old = (t - 2) % 3 */
+        if (a)
+            for (r = 0; r < J->nr; r++) {
+                X[cur][r] = X0[r];
+                plan_slice(&J->P[r], t, cs, &g_pipe[cur][r]);
+                X[cur][r].P = &g_pipe[cur][r];
+                X[cur][r].pool = c->pool + (t & 1) * region + off[r];
+            }
+        /* slice t-2's combine is done before its blocks leave and before
+         * slice t reuses its staging region */
+        if (dist && hipStreamWaitEvent(st, c->pev[2 + (int)(t & 1)], 0) != hipSuccess) return MPI_ERR_OTHER;
+        for (r = 0; r < J->nr; r++) {
+            mvx_xport *x = &J->t[r];
+            if ((rc = x->start(x))) return rc;
+            if (a && (rc = exec_phase_a(&X[cur][r], x, st))) return rc;
+            if (dist && (rc = exec_phase_c(&X[old][r], x, st))) return rc;
+            if ((rc = x->end(x))) return rc;
+        }
+        if (J->t[0].lb && (rc = lb_flush(J->t[0].lb, st))) return rc;
+        if (!a) continue;
+        if (hipEventRecord(c->pev[t & 1], st) != hipSuccess ||
+            hipStreamWaitEvent(c->cstream, c->pev[t & 1], 0) != hipSuccess)
+            return MPI_ERR_OTHER;
+        for (q = 0; q < J->nr; q++)
+            if ((rc = exec_phase_b(&X[cur][q], c->cstream))) return rc;
+        if (hipEventRecord(c->pev[2 + (int)(t & 1)], c->cstream) != hipSuccess) return MPI_ERR_OTHER;
+    }
+    return MPI_SUCCESS;
+}
+
+/* COLL: a regular plan -- every rank holds p equal blocks in rank order and
+ * combines block `rank` -- exchanges with ncclAllToAll and (Allreduce)
+ * distributes with an in-place ncclAllGather instead of grouped send /
+ * receive.  Every rank sees the same count and size, so all ranks choose
+ * the same variant. */
+static int coll_regular(const mvx_plan *P, long *blk)
+{
+    const long b = P->c_cnt;
+    int s;
+    if (P->p < 2 || !P->has_combine || b <= 0 || P->c_dst_tmp) return 0;
+    if (P->coll != MVX_COLL_ALLREDUCE && P->coll != MVX_COLL_REDUCE_SCATTER) return 0;
+    if (P->count != b * P->p || P->c_src_off != b * P->rank) return 0;
+    if (P->c_dst_off != (P->coll == MVX_COLL_ALLREDUCE ? b * P->rank : 0)) return 0;
+    for (s = 0; s < P->p; s++) {
+        if (s == P->rank) continue;
+        if (P->a_send[s].off != b * s || P->a_send[s].cnt != b) return 0;
+        if (P->a_recv[s].off != b * P->rank || P->a_recv[s].cnt != b) return 0;
+        if (P->coll == MVX_COLL_ALLREDUCE) {
+            if (P->b_send[s].off != b * P->rank || P->b_send[s].cnt != b) return 0;
+            if (P->b_recv[s].off != b * s || P->b_recv[s].cnt != b) return 0;
+        } else if (P->b_send[s].cnt || P->b_recv[s].cnt) {
+            return 0;
+        }
+    }
+    *blk = b;
+    return 1;
+}
+
+static int run_device_coll(mvx_comm_t *c, const job_t *J, long b, hipStream_t st)
+{
+    const mvx_plan *P = &J->P[0];
+    const size_t bb = (size_t)(b * P->esize);
+    const char *leafp[MVX_MAXP];
+    rank_exec_t X;
+    scratch_t S;
+    size_t stage;
+    int s, rc;
+    X.P = P; X.c = c; X.sendbuf = J->send[0]; X.recvbuf = J->recv[0];
+    stage = al256(bb * (size_t)P->p);
+    X.wide_n = wide_temps(P);
+    X.wide_slot = al256(bb + SLOT_STAGGER);
+    if ((rc = grow(&c->pool, &c->pool_bytes, stage + X.wide_slot * (size_t)X.wide_n))) return rc;
+    if (ncclAllToAll(J->send[0], c->pool, bb, ncclUint8, c->nccl, st) != ncclSuccess) return MPI_ERR_OTHER;
+    for (s = 0; s < P->p; s++)
+        leafp[s] = s == P->rank ? J->send[0] + (size_t)P->rank * bb : c->pool + (size_t)s * bb;
+    S.base = c->pool + stage; S.slot = X.wide_slot; S.used = 0; S.cap = X.wide_n;
+    if ((rc = combine(c, P, leafp, J->recv[0] + P->c_dst_off * P->esize, &S, st))) return rc;
+    if (P->coll == MVX_COLL_ALLREDUCE &&
+        ncclAllGather(J->recv[0] + (size_t)P->rank * bb, J->recv[0], bb, ncclUint8, c->nccl, st) != ncclSuccess)
+        return MPI_ERR_OTHER;
+    return MPI_SUCCESS;
+}
+
+/* all buffers in HBM */
+static int run_device(mvx_comm_t *c, const job_t *J, hipStream_t st)
+{
+    long blk;
+    if (c->exch == MVX_EXCH_PIPE) return run_device_pipe(c, J, st);
+    if (c->exch == MVX_EXCH_COLL && J->nr == 1 && J->t[0].nccl && J->P[0].opkind == MVX_OPKIND_PREDEFINED &&
+        coll_regular(&J->P[0], &blk))
+        return run_device_coll(c, J, blk, st);
+    return run_device_plain(c, J, st);
 }
 
 /* ---- host buffers: a sliced pipeline ------------------------------------
@@ -1006,7 +1243,6 @@ typedef struct {
     long cs;                                   /* slice length, elements */
 } stage_job_t;
 
-static size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 /* slice i in: host -> device for every host send buffer */
 static int stage_in(stage_job_t *S, const mvx_plan *Q, long i, hipStream_t st)
@@ -1217,8 +1453,14 @@ static int run(mvx_comm_t *c, const call_t *k, hipStream_t st, int blocking)
     if (verdict) return verdict;
 
     memset(&t, 0, sizeof t);
-    t.start = nc_start; t.end = nc_end; t.send = nc_send; t.recv = nc_recv;
-    t.nccl = c->nccl; t.me = c->rank;
+    if (c->has_ops) {
+        t.start = op_start; t.end = op_end; t.send = op_send; t.recv = op_recv;
+        t.ops = &c->ops; t.st = st;
+    } else {
+        t.start = nc_start; t.end = nc_end; t.send = nc_send; t.recv = nc_recv;
+        t.nccl = c->nccl;
+    }
+    t.me = c->rank;
     J.nr = 1;
     J.P = &P;
     J.send[0] = k->sendbuf;

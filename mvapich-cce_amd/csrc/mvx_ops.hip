@@ -401,9 +401,31 @@ namespace mvx {
 
 typedef void (*KFn)(const Params);
 
+// The launched template as rocprofv3 names it ("k_combine<2, float, 2, 4,
+// 1>"), from the compiler's own spelling of the template arguments, so
+// profiles and PMC summaries can be matched to what actually ran.
+template <int O, typename T, int KMAX, int U, int NT>
+static const char *ksym()
+{
+    static char buf[160];
+    if (!buf[0]) {
+        const char *pf = __PRETTY_FUNCTION__;
+        const char *t = strstr(pf, "T = ");
+        const char *e = t ? strstr(t, ", KMAX") : nullptr;
+        if (t && e)
+            snprintf(buf, sizeof buf, "k_combine<%d, %.*s, %d, %d, %d>", O, (int)(e - t - 4), t + 4, KMAX, U, NT);
+        else
+            snprintf(buf, sizeof buf, "k_combine<%d, ?, %d, %d, %d>", O, KMAX, U, NT);
+    }
+    return buf;
+}
+
+typedef const char *(*SymFn)();
+
 struct KSet {
     const void *apply[2];  // KMAX 2 (k <= 2), 4 chunks in flight per lane; [NT]
     const void *prog[2];   // KMAX 8 combine program
+    SymFn apply_sym[2], prog_sym[2];
     int prog_unroll;       // its chunks in flight per lane
     int esize;
     int chunk;             // bytes per chunk (16, or the element if wider)
@@ -416,6 +438,8 @@ static KSet kset(const char *name)
     KSet s;
     s.apply[0] = (const void *)&k_combine<O, T, 2, 4, 0>;
     s.apply[1] = (const void *)&k_combine<O, T, 2, 4, 1>;
+    s.apply_sym[0] = &ksym<O, T, 2, 4, 0>;
+    s.apply_sym[1] = &ksym<O, T, 2, 4, 1>;
     // chunks in flight per lane, measured (tools/bench_kernels.py, A/B in one
     // box): 4-byte elements 2 (config-3 tree 52.4 vs 53.0 us), 8-byte
     // elements 1 (config-4 chain 217 vs 234 us, config-5 MAXLOC 102 vs
@@ -424,6 +448,8 @@ static KSet kset(const char *name)
     constexpr int UP = sizeof(T) == 4 ? 2 : 1;
     s.prog[0] = (const void *)&k_combine<O, T, MVX_COMBINE_KMAX, UP, 0>;
     s.prog[1] = (const void *)&k_combine<O, T, MVX_COMBINE_KMAX, UP, 1>;
+    s.prog_sym[0] = &ksym<O, T, MVX_COMBINE_KMAX, UP, 0>;
+    s.prog_sym[1] = &ksym<O, T, MVX_COMBINE_KMAX, UP, 1>;
     s.prog_unroll = UP;
 
     s.esize = (int)sizeof(T);
@@ -626,6 +652,7 @@ static int g_block_cap = 1 << 20;
 static long g_nt_min_bytes = 64L << 20;
 static const char *g_last = "";
 static char g_last_buf[96];
+static const char *g_last_sym = "";
 
 static void init_env()
 {
@@ -638,8 +665,8 @@ static void init_env()
     if (e && atoi(e) > 0) g_block_cap = atoi(e);
 }
 
-static int launch(const KSet *ks, const void *const fns[2], int unroll, Params &P,
-                  hipStream_t stream)
+static int launch(const KSet *ks, const void *const fns[2], const SymFn syms[2], int unroll,
+                  Params &P, hipStream_t stream)
 {
     init_env();
     int nleaves = 0;
@@ -673,6 +700,7 @@ static int launch(const KSet *ks, const void *const fns[2], int unroll, Params &
     hipError_t e = hipLaunchKernel(fn, dim3(blocks), dim3(256), args, 0, stream);
     snprintf(g_last_buf, sizeof g_last_buf, "%s_k%d%s", ks->name, P.k, nt ? "_nt" : "");
     g_last = g_last_buf;
+    g_last_sym = syms[nt]();
     return e == hipSuccess ? MPI_SUCCESS : MPI_ERR_OTHER;
 }
 
@@ -785,7 +813,7 @@ extern "C" int mvx_op_apply(int op, int dtype, const void *in, void *inout,
     P.dst = (char *)inout;
     P.n = (long)n;
     P.k = 2;
-    return launch(ks, ks->apply, 4, P, (hipStream_t)stream);
+    return launch(ks, ks->apply, ks->apply_sym, 4, P, (hipStream_t)stream);
 }
 
 extern "C" int mvx_op_program(int op, int dtype, const void *const *srcs,
@@ -816,9 +844,9 @@ extern "C" int mvx_op_program(int op, int dtype, const void *const *srcs,
     if (k <= 2) {
         /* the only programs over <= 2 leaves: nothing, or y0 op y1 */
         if (k == 2 && !(tree_mask & 1u) && !(chain_mask & 2u)) return MPI_ERR_ARG;
-        return launch(ks, ks->apply, 4, P, (hipStream_t)stream);
+        return launch(ks, ks->apply, ks->apply_sym, 4, P, (hipStream_t)stream);
     }
-    return launch(ks, ks->prog, ks->prog_unroll, P, (hipStream_t)stream);
+    return launch(ks, ks->prog, ks->prog_sym, ks->prog_unroll, P, (hipStream_t)stream);
 }
 
 extern "C" unsigned mvx_tree_mask(int k)
@@ -856,3 +884,5 @@ extern "C" void mvx_hip_set_launch(int block_cap, int nt_min_bytes_log2)
 }
 
 extern "C" const char *mvx_hip_last_kernel(void) { return g_last; }
+
+extern "C" const char *mvx_hip_last_kernel_symbol(void) { return g_last_sym; }

@@ -1,0 +1,134 @@
+#!/usr/bin/env python3
+"""TEST HELPER: one rank of a multi-process collective test.
+
+Launched once per rank by tests/test_gpu_multiproc.py (fresh processes, no
+GPU state inherited).  Every rank builds every rank's inputs from seeds, runs
+the collectives through its libmvx.so communicator and compares its own
+result with the oracle's replay of the reference schedule
+(oracle/coll_sim.c) computed over all ranks' inputs.  Writes a JSON report.
+
+  mp_worker.py RANK WORLD PORT OUT.json TRANSPORT(host|rccl) SUITE(small|full)
+"""
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+sys.path[:0] = [ROOT, HERE]
+
+
+def main():
+    rank, world, port, out, transport, suite = (int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4],
+                                                 sys.argv[5], sys.argv[6])
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+    import importlib
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import mvxtest as T
+    from oracle import oracle as O
+    mvx = importlib.import_module("mvapich-cce_amd")
+    from importlib import import_module
+    tp = import_module("mvapich-cce_amd.transport")
+
+    ndev = torch.cuda.device_count()
+    dev = rank % ndev if transport == "host" else rank
+    torch.cuda.set_device(dev)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    if transport == "host":
+        comm = mvx.Comm.from_transport(tp.TorchP2PTransport(), dev)
+    else:
+        comm = mvx.Comm.from_torch_distributed(dev)
+    report = {"rank": rank, "checked": 0, "fails": []}
+
+    def inputs(dtype, tot, fill):
+        if fill is None:
+            return [T.rand_vec(dtype, tot, 1000 * world + 17 * r + tot + dtype) for r in range(world)]
+        out = []
+        for r in range(world):          # SURVEY.md 8(d) distributions (oracle/cpu_ops.c orc_fill)
+            a = np.empty(tot, T.np_dtype(dtype))
+            O.fill(a, tot, fill, r)
+            out.append(a)
+        return out
+
+    def check(coll, dtype, op, n_or_cnts, where, root=0, tag="", fill=None):
+        E = mvx.dtype_info(dtype)[0]
+        cnts = n_or_cnts if coll == "rs" else None
+        tot = sum(cnts) if cnts else n_or_cnts
+        S = inputs(dtype, tot, fill)
+        nrecv = cnts[rank] if cnts else tot
+        if where == "device":
+            s = T.to_dev(S[rank])
+            r = torch.zeros(max(nrecv, 1) * E, dtype=torch.uint8, device="cuda")
+        else:
+            s = T.clone(S[rank]).view(np.uint8)
+            r = np.zeros(max(nrecv, 1) * E, np.uint8)
+        if coll == "ar":
+            rc = mvx.MPI_Allreduce(s, r, tot, dtype, op, comm)
+        elif coll == "red":
+            rc = mvx.MPI_Reduce(s, r, tot, dtype, op, root, comm)
+        elif coll == "scan":
+            rc = mvx.MPI_Scan(s, r, tot, dtype, op, comm)
+        else:
+            rc = mvx.MPI_Reduce_scatter(s, r, cnts, dtype, op, comm)
+        got = r if isinstance(r, np.ndarray) else T.from_dev(r)
+        R0 = [np.zeros(max(cnts[q] if cnts else tot, 1), S[0].dtype) for q in range(world)]
+        s8, r8 = [x.view(np.uint8) for x in S], [x.view(np.uint8) for x in R0]
+        if coll == "ar":
+            rref = O.allreduce(s8, r8, tot, dtype, op)
+        elif coll == "red":
+            rref = O.reduce(s8, r8, tot, dtype, op, root)
+        elif coll == "scan":
+            rref = O.scan(s8, r8, tot, dtype, op)
+        else:
+            rref = O.reduce_scatter(s8, r8, cnts, dtype, op)
+        report["checked"] += 1
+        ok = rc == rref[rank]
+        if ok and rc == 0 and (coll != "red" or rank == root):
+            try:
+                T.assert_same(op, dtype, got[: nrecv * E], R0[rank][:nrecv], typemap_only=True)
+            except AssertionError as e:
+                ok = False
+                tag += " " + str(e)[:200]
+        if not ok:
+            report["fails"].append([coll, dtype, op, tot, where, root, rc, rref[rank], tag])
+
+    modes = [("p2p", mvx.EXCH_P2P, 0), ("pipe", mvx.EXCH_PIPE, 3)]
+    if transport == "rccl":
+        modes.append(("coll", mvx.EXCH_COLL, 0))
+    if suite == "small":
+        cases = [(102, 10), (100, 10), (111, 17), (105, 8), (110, 18), (103, 6)]
+        for name, mode, sl in modes:
+            assert comm.set_exchange(mode, sl) == 0
+            for op, dtype in cases:
+                for where in ("device", "host"):
+                    for n in (1, 10, 4097, 70001, 300000):
+                        check("ar", dtype, op, n, where, tag=name)
+                    for n in (5, 70001):
+                        check("red", dtype, op, n, where, root=world - 1, tag=name)
+                    for base in (3, 40000, 140000):
+                        check("rs", dtype, op, [base + (q % 2) for q in range(world)], where, tag=name)
+                    check("scan", dtype, op, 5000, where, tag=name)
+    else:
+        # the BASELINE multi-GPU shapes at full size: C3, C4 (p = 4 in the
+        # config; any p here), C5
+        for name, mode, sl in modes:
+            assert comm.set_exchange(mode, sl) == 0
+            check("ar", 10, 102, 64 << 20, "device", tag=name + " c3", fill=0)
+            check("rs", 8, 105, [(1 << 27) // world] * world, "device", tag=name + " c4", fill=2)
+            check("ar", 17, 111, 64 << 20, "device", tag=name + " c5", fill=4)
+            torch.cuda.empty_cache()
+    if transport == "host":
+        report["transport_errors"] = comm.transport.errors
+    comm.free()
+    dist.barrier()
+    dist.destroy_process_group()
+    with open(out, "w") as f:
+        json.dump(report, f)
+
+
+if __name__ == "__main__":
+    main()
