@@ -99,19 +99,32 @@ int MPI_Scan(void *sendbuf, void *recvbuf, int count, MPI_Datatype datatype,
 int MPI_Op_create(MPI_User_function *function, int commute, MPI_Op *op);
 int MPI_Op_free(MPI_Op *op);
 
-/* Derived datatypes, contiguous only (include/mpi.h:369-385;
- * src/pt2pt/type_contig.c, type_commit.c, type_free.c, type_extent.c,
- * type_size.c): usable with every collective here -- with MPI_Op_create ops
- * (the user function gets the derived handle, as in the reference), and with
- * MPI_MAXLOC / MPI_MINLOC when the type is a count-2 contiguous pair over
- * INT, LONG, LONG_LONG_INT, SHORT, CHAR, FLOAT, DOUBLE or LONG_DOUBLE
- * (global_ops.c:1387-1503 / 1625-1740); any other predefined op on a derived
- * type is the reference's 329.  Table in libmvx_hip.so (mvx_hip.h). */
+/* Derived datatypes (include/mpi.h:369-385; src/pt2pt/type_*.c; the type
+ * engine is libmvx_hip.so's, include/mvx_hip.h): usable with every
+ * collective here -- with MPI_Op_create ops (the user function gets the
+ * derived handle and buffers laid out by extent, as in the reference), and
+ * with MPI_MAXLOC / MPI_MINLOC on a count-2 contiguous pair type or on a
+ * struct type read as its first member's C pair struct (global_ops.c:
+ * 1280-1503, 1520-1740); any other predefined op on a derived type is the
+ * reference's 329.  Types whose type map has holes move packed (type-map
+ * bytes only) and are unpacked into recvbuf, so bytes outside the type map
+ * are never written. */
 int MPI_Type_contiguous(int count, MPI_Datatype oldtype, MPI_Datatype *newtype);
+int MPI_Type_vector(int count, int blocklen, int stride, MPI_Datatype oldtype, MPI_Datatype *newtype);
+int MPI_Type_hvector(int count, int blocklen, MPI_Aint stride, MPI_Datatype oldtype,
+                     MPI_Datatype *newtype);
+int MPI_Type_indexed(int count, int *blocklens, int *indices, MPI_Datatype oldtype,
+                     MPI_Datatype *newtype);
+int MPI_Type_hindexed(int count, int *blocklens, MPI_Aint *indices, MPI_Datatype oldtype,
+                      MPI_Datatype *newtype);
+int MPI_Type_struct(int count, int *blocklens, MPI_Aint *indices, MPI_Datatype *types,
+                    MPI_Datatype *newtype);
 int MPI_Type_commit(MPI_Datatype *datatype);
 int MPI_Type_free(MPI_Datatype *datatype);
 int MPI_Type_extent(MPI_Datatype datatype, MPI_Aint *extent);
 int MPI_Type_size(MPI_Datatype datatype, int *size);
+int MPI_Type_lb(MPI_Datatype datatype, MPI_Aint *displacement);
+int MPI_Type_ub(MPI_Datatype datatype, MPI_Aint *displacement);
 
 /* A user op whose function runs on the device: `function` enqueues
  * inoutvec[i] = invec[i] op inoutvec[i], i < len, on `stream` (a
@@ -313,6 +326,10 @@ typedef struct mvx_plan {
      * kernels never see a swap). */
     int tree_swap;
     unsigned long long chain_swap;
+    /* the datatype's type map has holes (mvx_type_layout dense == 0): every
+     * range moves packed type-map bytes, esize = MPI_Type_size; the combine
+     * unpacks its leaves to the extent layout the op sees */
+    int packed;
 } mvx_plan;
 
 /* The single-launch masks (mvx_op_program) of a plan's program when

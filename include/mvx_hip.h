@@ -46,30 +46,76 @@ extern "C" {
 
 /* 1 if a device kernel exists for (op, dtype); 0 otherwise. */
 int mvx_op_supported(int op, int dtype);
+/* Bytes of one element as the (op, dtype) kernel reads it (the C pair
+ * struct for MAXLOC / MINLOC on a struct type), or 0 if undefined. */
+int mvx_op_element_size(int op, int dtype);
 
 /* Bytes per element (the datatype extent) on the device path, or 0. */
 int mvx_dtype_extent(int dtype);
 
-/* Derived datatypes: MPI_Type_contiguous (src/pt2pt/type_contig.c:52-187).
- * A contiguous type over a contiguous type that has an old type (MPI_2INT or
- * another derived contiguous type) is flattened as the reference does
- * (:139-146): contig(1, MPI_2INT) is contig(2, MPI_INT).  The ops follow
- * global_ops.c: only MAXLOC / MINLOC on a count-2 contiguous type over INT,
- * LONG, LONG_LONG_INT, SHORT, CHAR, FLOAT, DOUBLE or LONG_DOUBLE are defined
- * (stride-2 {value, loc} pairs of the base type, 1387-1503 / 1625-1740);
- * every other (op, derived type) is 329, as each op's `switch (dte_type)`
- * has no MPIR_CONTIG case.  Handles are MVX_TYPE_DERIVED_BASE + slot. */
+/* Derived datatypes (the reference's src/pt2pt type constructors, with its
+ * bounds rules: MPI_LB / MPI_UB markers, struct alignment to the largest
+ * member, vector -> hvector and indexed -> hindexed reductions, the empty
+ * type for count 0):
+ *   mvx_type_contiguous  type_contig.c:52-187 (MPI_2INT and contiguous old
+ *                        types flattened, :139-146)
+ *   mvx_type_vector      type_vec.c:44-110
+ *   mvx_type_hvector     type_hvec.c:55-175
+ *   mvx_type_indexed     type_ind.c:74-134
+ *   mvx_type_hindexed    type_hind.c:57-200
+ *   mvx_type_struct      type_struct.c:106-330
+ *   mvx_type_commit      type_commit.c:41-143
+ *   mvx_type_free        type_free.c:60-105
+ * The ops follow global_ops.c: MAXLOC / MINLOC are defined on a count-2
+ * contiguous type over INT, LONG, LONG_LONG_INT, SHORT, CHAR, FLOAT, DOUBLE
+ * or LONG_DOUBLE (stride-2 {value, loc}, 1387-1503 / 1625-1740) and on a
+ * struct type by the type of its first member (read as that type's C pair
+ * struct, 1280-1384 / 1520-1620); every other (op, derived type) is 329.
+ * Handles are MVX_TYPE_DERIVED_BASE + slot.
+ * Return codes: 0, MPI_ERR_COUNT, MPI_ERR_ARG, MPI_ERR_TYPE, 323 (null or
+ * unknown old type), MPI_ERR_INTERN (table full); a negative value
+ * MVX_SETMSG(class, kind) is a code the reference creates with
+ * MPIR_Err_setmsg (the MPI_Type_* wrappers of libmvx.so add the error-ring
+ * position). */
 #define MVX_TYPE_DERIVED_BASE 256
 #define MVX_TYPE_DERIVED_MAX  256
-/* 0, MPI_ERR_COUNT (count < 0), 323 (null or unknown oldtype),
- * MPI_ERR_TYPE (MPI_LB / MPI_UB), MPI_ERR_INTERN (table full) */
+#define MVX_SETMSG(cls, kind) (-((cls) | ((kind) << 6)))
+#define MVX_ERR_KIND_TYPE_ARRAY_NULL 13   /* mpi_error.h:143 */
+#define MVX_ERR_KIND_ARG_ARRAY_VAL   31   /* mpi_error.h:212 */
 int mvx_type_contiguous(int count, int oldtype, int *newtype);
+int mvx_type_vector(int count, int blocklen, int stride, int oldtype, int *newtype);
+int mvx_type_hvector(int count, int blocklen, long stride, int oldtype, int *newtype);
+int mvx_type_indexed(int count, const int *blocklens, const int *indices, int oldtype, int *newtype);
+int mvx_type_hindexed(int count, const int *blocklens, const long *indices, int oldtype, int *newtype);
+int mvx_type_struct(int count, const int *blocklens, const long *indices, const int *types,
+                    int *newtype);
+/* 0, or 323 for a null / unknown handle */
+int mvx_type_commit(int type);
 /* 0 (and *type = MPI_DATATYPE_NULL), 323 (null / unknown), 579 (predefined) */
 int mvx_type_free(int *type);
-/* Any handle, basic or derived: its old type after flattening (the handle
- * itself for a basic type; MPI_INT for MPI_2INT), replication count (1 for
- * a basic type), extent and size in bytes.  0 or MPI_ERR_TYPE. */
+/* Any handle, basic or derived: its old type (the handle itself for a basic
+ * type; MPI_INT for MPI_2INT; the flattened old type of a contiguous type;
+ * the first member's type of a struct), replication count, extent and size
+ * in bytes.  0 or MPI_ERR_TYPE. */
 int mvx_type_describe(int type, int *oldtype, int *count, long *extent, long *size);
+/* The reference's dte_type (MVX_TK_*), whether elements move whole (dense:
+ * the type map covers the extent from offset 0 -- basic types, the padded
+ * pair structs, contiguous types of them) or packed, the bounds, and the
+ * lowest / one-past-highest byte of one element's type map. */
+#define MVX_TK_BASIC    0
+#define MVX_TK_CONTIG   1
+#define MVX_TK_HVECTOR  2
+#define MVX_TK_HINDEXED 3
+#define MVX_TK_STRUCT   4
+#define MVX_TK_UB       5
+#define MVX_TK_LB       6
+int mvx_type_layout(int type, int *kind, int *dense, long *lb, long *ub, long *span_lo, long *span_hi);
+/* count elements between the type's layout at `origin` (element i at
+ * origin + i * extent + type-map offsets) and the packed form (type-map
+ * bytes only, size bytes per element), on the device, stream-ordered.
+ * Unpacking writes type-map bytes only. */
+int mvx_type_pack(int type, const void *origin, void *packed, size_t count, void *hip_stream);
+int mvx_type_unpack(int type, const void *packed, void *origin, size_t count, void *hip_stream);
 
 /* inout[i] = in[i] op inout[i], i < n.  Returns MPI_SUCCESS, 329 for an
  * undefined (op, type) pair (as MPIR_ERR_OP_NOT_DEFINED), MPI_ERR_OP for an

@@ -64,6 +64,7 @@ class Plan(ctypes.Structure):
         ("c_src_off", ctypes.c_long), ("c_cnt", ctypes.c_long), ("c_dst_off", ctypes.c_long),
         ("b_send", Range * MAXP), ("b_recv", Range * MAXP),
         ("opkind", ctypes.c_int), ("tree_swap", ctypes.c_int), ("chain_swap", ctypes.c_ulonglong),
+        ("packed", ctypes.c_int),
     ]
 
     def masks(self):
@@ -170,6 +171,17 @@ def _load():
     _hip.mvx_type_free.argtypes = [pi]
     _hip.mvx_type_describe.argtypes = [i, pi, pi, pl, pl]
     c.MPI_Type_contiguous.argtypes = [i, i, pi]
+    c.MPI_Type_vector.argtypes = [i, i, i, i, pi]
+    c.MPI_Type_hvector.argtypes = [i, i, ctypes.c_long, i, pi]
+    c.MPI_Type_indexed.argtypes = [i, pi, pi, i, pi]
+    c.MPI_Type_hindexed.argtypes = [i, pi, pl, i, pi]
+    c.MPI_Type_struct.argtypes = [i, pi, pl, pi, pi]
+    c.MPI_Type_lb.argtypes = [i, pl]
+    c.MPI_Type_ub.argtypes = [i, pl]
+    _hip.mvx_type_layout.argtypes = [i, pi, pi, pl, pl, pl, pl]
+    _hip.mvx_type_pack.argtypes = [i, vp, vp, sz, vp]
+    _hip.mvx_type_unpack.argtypes = [i, vp, vp, sz, vp]
+    _hip.mvx_op_element_size.argtypes = [i, i]
     c.MPI_Type_commit.argtypes = [pi]
     c.MPI_Type_free.argtypes = [pi]
     c.MPI_Type_extent.argtypes = [i, pl]

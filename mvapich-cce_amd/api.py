@@ -14,6 +14,8 @@ __all__ = [
     "MPI_Allreduce", "MPI_Reduce", "MPI_Reduce_scatter", "MPI_Scan", "MPI_Op_create", "MPI_Op_free", "op_create_device",
     "MPIR_call", "op_errno", "last_kernel", "last_kernel_symbol", "set_launch",
     "MPI_Type_contiguous", "MPI_Type_commit", "MPI_Type_free", "MPI_Type_extent", "MPI_Type_size",
+    "MPI_Type_vector", "MPI_Type_hvector", "MPI_Type_indexed", "MPI_Type_hindexed", "MPI_Type_struct",
+    "MPI_Type_lb", "MPI_Type_ub", "type_layout", "type_pack", "type_unpack",
 ]
 
 
@@ -279,6 +281,74 @@ def MPI_Type_contiguous(count, oldtype):
     h = ctypes.c_int()
     rc = coll().MPI_Type_contiguous(count, oldtype, ctypes.byref(h))
     return rc, h.value
+
+
+def _iarr(vals, ct=ctypes.c_int):
+    return (ct * max(len(vals), 1))(*vals)
+
+
+def MPI_Type_vector(count, blocklen, stride, oldtype):
+    """Returns (rc, new handle)."""
+    h = ctypes.c_int()
+    rc = coll().MPI_Type_vector(count, blocklen, stride, oldtype, ctypes.byref(h))
+    return rc, h.value
+
+
+def MPI_Type_hvector(count, blocklen, stride_bytes, oldtype):
+    h = ctypes.c_int()
+    rc = coll().MPI_Type_hvector(count, blocklen, stride_bytes, oldtype, ctypes.byref(h))
+    return rc, h.value
+
+
+def MPI_Type_indexed(count, blocklens, indices, oldtype):
+    h = ctypes.c_int()
+    rc = coll().MPI_Type_indexed(count, _iarr(blocklens), _iarr(indices), oldtype, ctypes.byref(h))
+    return rc, h.value
+
+
+def MPI_Type_hindexed(count, blocklens, byte_indices, oldtype):
+    h = ctypes.c_int()
+    rc = coll().MPI_Type_hindexed(count, _iarr(blocklens), _iarr(byte_indices, ctypes.c_long), oldtype,
+                                  ctypes.byref(h))
+    return rc, h.value
+
+
+def MPI_Type_struct(count, blocklens, byte_indices, types):
+    h = ctypes.c_int()
+    rc = coll().MPI_Type_struct(count, _iarr(blocklens), _iarr(byte_indices, ctypes.c_long), _iarr(types),
+                                ctypes.byref(h))
+    return rc, h.value
+
+
+def MPI_Type_lb(datatype):
+    v = ctypes.c_long()
+    rc = coll().MPI_Type_lb(datatype, ctypes.byref(v))
+    return rc, v.value
+
+
+def MPI_Type_ub(datatype):
+    v = ctypes.c_long()
+    rc = coll().MPI_Type_ub(datatype, ctypes.byref(v))
+    return rc, v.value
+
+
+def type_layout(datatype):
+    """dict(kind, dense, lb, ub, span_lo, span_hi) from mvx_type_layout."""
+    k, d = ctypes.c_int(), ctypes.c_int()
+    lb, ub, lo, hi = ctypes.c_long(), ctypes.c_long(), ctypes.c_long(), ctypes.c_long()
+    rc = hip().mvx_type_layout(datatype, ctypes.byref(k), ctypes.byref(d), ctypes.byref(lb), ctypes.byref(ub),
+                               ctypes.byref(lo), ctypes.byref(hi))
+    if rc:
+        raise ValueError("mvx_type_layout rc=%d" % rc)
+    return dict(kind=k.value, dense=d.value, lb=lb.value, ub=ub.value, span_lo=lo.value, span_hi=hi.value)
+
+
+def type_pack(datatype, origin, packed, count, stream=None):
+    return hip().mvx_type_pack(datatype, addr(origin), addr(packed), count, stream_handle(stream))
+
+
+def type_unpack(datatype, packed, origin, count, stream=None):
+    return hip().mvx_type_unpack(datatype, addr(packed), addr(origin), count, stream_handle(stream))
 
 
 def MPI_Type_commit(datatype):

@@ -68,6 +68,8 @@ typedef struct {
     size_t upool_bytes;
     char *uhost;         /* user-op scratch: pinned host (MPI_User_functions) */
     size_t uhost_bytes;
+    char *xpool;         /* extent-layout scratch of packed (holey) datatypes */
+    size_t xpool_bytes;
     mvx_tuning tune;     /* device flavour + knobs (mvx_coll.h) */
     int shmem_block;     /* claimed shmem collective block, -1 = none */
     int exch, exch_slices;      /* exchange variant, MVX_EXCH_* (mvx_coll.h) */
@@ -284,6 +286,7 @@ int mvx_comm_free(MPI_Comm *comm)
     if (c->hpool) hipFree(c->hpool);
     if (c->upool) hipFree(c->upool);
     if (c->uhost) hipHostFree(c->uhost);
+    if (c->xpool) hipFree(c->xpool);
     if (c->cstream) {
         int i;
         hipStreamDestroy(c->cstream);
@@ -440,18 +443,52 @@ int mvx_op_create_device(MVX_Device_function *function, int commute, MPI_Op *op)
 
 /* ---- derived datatypes (the table is libmvx_hip.so's) ------------------ */
 
+/* the type engine's codes: a negative value is MVX_SETMSG(class, kind), a
+ * code the reference makes with MPIR_Err_setmsg (error ring position added) */
+static int type_rc(int rc)
+{
+    if (rc >= 0) return rc;
+    rc = -rc;
+    return setmsg_code(rc & ((1 << MVX_ERR_CLASS_BITS) - 1), rc >> MVX_ERR_CLASS_BITS);
+}
+
 int MPI_Type_contiguous(int count, MPI_Datatype old, MPI_Datatype *newtype)
 {
-    return mvx_type_contiguous(count, old, newtype);
+    return type_rc(mvx_type_contiguous(count, old, newtype));
+}
+
+int MPI_Type_vector(int count, int blocklen, int stride, MPI_Datatype old, MPI_Datatype *newtype)
+{
+    return type_rc(mvx_type_vector(count, blocklen, stride, old, newtype));
+}
+
+int MPI_Type_hvector(int count, int blocklen, MPI_Aint stride, MPI_Datatype old, MPI_Datatype *newtype)
+{
+    return type_rc(mvx_type_hvector(count, blocklen, stride, old, newtype));
+}
+
+int MPI_Type_indexed(int count, int *blocklens, int *indices, MPI_Datatype old, MPI_Datatype *newtype)
+{
+    return type_rc(mvx_type_indexed(count, blocklens, indices, old, newtype));
+}
+
+int MPI_Type_hindexed(int count, int *blocklens, MPI_Aint *indices, MPI_Datatype old, MPI_Datatype *newtype)
+{
+    return type_rc(mvx_type_hindexed(count, blocklens, indices, old, newtype));
+}
+
+int MPI_Type_struct(int count, int *blocklens, MPI_Aint *indices, MPI_Datatype *types, MPI_Datatype *newtype)
+{
+    return type_rc(mvx_type_struct(count, blocklens, indices, types, newtype));
 }
 
 int MPI_Type_commit(MPI_Datatype *datatype)   /* type_commit.c:41-143 */
 {
-    if (!datatype || mvx_type_describe(*datatype, NULL, NULL, NULL, NULL)) return MVX_ERR_TYPE_NULL;
-    return MPI_SUCCESS;   /* contiguous types need no flattening */
+    if (!datatype) return MVX_ERR_TYPE_NULL;
+    return type_rc(mvx_type_commit(*datatype));
 }
 
-int MPI_Type_free(MPI_Datatype *datatype) { return mvx_type_free(datatype); }
+int MPI_Type_free(MPI_Datatype *datatype) { return type_rc(mvx_type_free(datatype)); }
 
 int MPI_Type_extent(MPI_Datatype datatype, MPI_Aint *extent)
 {
@@ -468,6 +505,24 @@ int MPI_Type_size(MPI_Datatype datatype, int *size)
     if (mvx_type_describe(datatype, NULL, NULL, NULL, &s)) return MVX_ERR_TYPE_NULL;
     if (!size) return MPI_ERR_ARG;
     *size = (int)s;
+    return MPI_SUCCESS;
+}
+
+int MPI_Type_lb(MPI_Datatype datatype, MPI_Aint *displacement)   /* type_lb.c */
+{
+    long lb;
+    if (mvx_type_layout(datatype, NULL, NULL, &lb, NULL, NULL, NULL)) return MVX_ERR_TYPE_NULL;
+    if (!displacement) return MPI_ERR_ARG;
+    *displacement = lb;
+    return MPI_SUCCESS;
+}
+
+int MPI_Type_ub(MPI_Datatype datatype, MPI_Aint *displacement)   /* type_ub.c */
+{
+    long ub;
+    if (mvx_type_layout(datatype, NULL, NULL, NULL, &ub, NULL, NULL)) return MVX_ERR_TYPE_NULL;
+    if (!displacement) return MPI_ERR_ARG;
+    *displacement = ub;
     return MPI_SUCCESS;
 }
 
@@ -524,7 +579,14 @@ static size_t slot_at(size_t cur, const void *like)
     return base + ((uintptr_t)like & 15);
 }
 
-#define NCCL_OK(x) do { if ((x) != ncclSuccess) return MPI_ERR_OTHER; } while (0)
+static size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+/* Consecutive staging slots are 4 KiB apart beyond their size: back-to-back
+ * equal-size shards put the same chunk of every leaf at the same DRAM
+ * interleave position, and the k-leaf combine then ran 5-6 % slower
+ * (tools/tune_combine_layout.py, profiles/r01/tune_combine_layout.jsonl:
+ * 53.9 vs 51.2 us for 8 x 32 MiB). */
+#define SLOT_STAGGER 4096
 
 /* ---- user ops: the combine program as a sequence of user calls --------
  * The reference hands a user function (*uop)(in, inout, &len, &type) its
@@ -562,12 +624,15 @@ static int seg_end(const mvx_plan *P, int q)
     return e;
 }
 
+/* The user function sees every operand at its origin (element i at
+ * origin + i * extent); the bytes it may touch are [origin + lo,
+ * origin + lo + region) -- the whole vector for a contiguous type. */
 static int combine_user(mvx_comm_t *c, const mvx_plan *P, const void *const *srcs,
-                        const void *const *fold, void *dst, hipStream_t st)
+                        const void *const *fold, void *dst, hipStream_t st, long lo, size_t region)
 {
     const mvx_op_t *o = user_op(P->op);
     const long n = P->c_cnt, E = P->esize;
-    const size_t bytes = (size_t)(n * E), slot = (bytes + 255) & ~(size_t)255;
+    const size_t slot = (region + 255) & ~(size_t)255;
     const int dev = o && o->dop;
     const hipMemcpyKind in_kind = dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
     char *y[MVX_MAXK] = {0}, *base;
@@ -576,11 +641,13 @@ static int combine_user(mvx_comm_t *c, const mvx_plan *P, const void *const *src
     if (dev) rc = grow(&c->upool, &c->upool_bytes, slot * (size_t)P->k * 2);
     else rc = grow_host(&c->uhost, &c->uhost_bytes, slot * (size_t)P->k * 2);
     if (rc) return rc;
-    base = dev ? c->upool : c->uhost;
+    base = (dev ? c->upool : c->uhost) - lo;   /* origins of the scratch slots */
     for (q = 0; q < P->k; q++) {
         y[q] = base + slot * (size_t)q;
-        if (hipMemcpyAsync(y[q], srcs[q], bytes, in_kind, st) != hipSuccess) return MPI_ERR_OTHER;
-        if (fold[q] && hipMemcpyAsync(base + slot * (size_t)(P->k + q), fold[q], bytes, in_kind, st) != hipSuccess)
+        if (hipMemcpyAsync(y[q] + lo, (const char *)srcs[q] + lo, region, in_kind, st) != hipSuccess)
+            return MPI_ERR_OTHER;
+        if (fold[q] && hipMemcpyAsync(base + slot * (size_t)(P->k + q) + lo, (const char *)fold[q] + lo, region,
+                                      in_kind, st) != hipSuccess)
             return MPI_ERR_OTHER;
     }
     if (!dev && hipStreamSynchronize(st) != hipSuccess) return MPI_ERR_OTHER;
@@ -606,7 +673,8 @@ static int combine_user(mvx_comm_t *c, const mvx_plan *P, const void *const *src
         else rc = user_step(o, b, a, n, (int)E, P->dtype, st);
         if (rc) return rc;
     }
-    if (hipMemcpyAsync(dst, y[0], bytes, dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, st) != hipSuccess)
+    if (hipMemcpyAsync((char *)dst + lo, y[0] + lo, region, dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
+                       st) != hipSuccess)
         return MPI_ERR_OTHER;
     /* the pinned scratch is reused by the next call */
     return (!dev && hipStreamSynchronize(st) != hipSuccess) ? MPI_ERR_OTHER : MPI_SUCCESS;
@@ -700,6 +768,70 @@ static int combine_wide(const mvx_plan *P, const void *const *srcs, const void *
     return chain_eval(P, heads, nh, dst, S, st);
 }
 
+/* ---- datatypes with holes (plan->packed) --------------------------------
+ * Leaves arrive packed (type-map bytes only).  The op sees the reference's
+ * layout -- count elements at the type's extent, as the (*uop) calls on
+ * tmp_buf / recvbuf do (intra_fns_new.c:5505-5512) -- so the combine
+ * unpacks every leaf into an extent-layout scratch slot (bytes outside the
+ * type map read as zero), runs the program there and packs the result. */
+static int combine_packed(mvx_comm_t *c, const mvx_plan *P, const void *const *srcs,
+                          const void *const *fold, void *dst, hipStream_t st)
+{
+    const long n = P->c_cnt;
+    const void *usrc[MVX_MAXK], *ufold[MVX_MAXK];
+    long ext, lo, hi, a, b;
+    size_t slot;
+    int q, j = 0, nf = 0, rc, wide = 0;
+    mvx_plan Q;
+    char *out;
+    if (mvx_type_describe(P->dtype, NULL, NULL, &ext, NULL) ||
+        mvx_type_layout(P->dtype, NULL, NULL, NULL, NULL, &lo, &hi))
+        return MPI_ERR_TYPE;
+    Q = *P;
+    Q.packed = 0;
+    Q.esize = (int)ext;
+    if (Q.opkind == MVX_OPKIND_PREDEFINED) {
+        /* the kernel reads n C pair structs from each origin: the reference's
+         * (*uop) calls on a struct type whose extent is not its first
+         * member's pair struct overlap elements, which no reordering of the
+         * calls reproduces -- refused */
+        if (mvx_op_element_size(P->op, P->dtype) != ext) return MPI_ERR_TYPE;
+        wide = wide_temps(&Q);
+    }
+    /* a slot covers the type map of n elements and the op's n * extent */
+    a = lo < 0 ? lo : 0;
+    b = (n - 1) * ext + hi;
+    if (b < n * ext) b = n * ext;
+    slot = al256((size_t)(b - a) + SLOT_STAGGER);
+    for (q = 0; q < P->k; q++) nf += fold[q] != NULL;
+    if ((rc = grow(&c->xpool, &c->xpool_bytes, slot * (size_t)(P->k + nf + 1 + wide)))) return rc;
+    if (hipMemsetAsync(c->xpool, 0, slot * (size_t)(P->k + nf + 1), st) != hipSuccess) return MPI_ERR_OTHER;
+    for (q = 0; q < P->k; q++) {
+        usrc[q] = c->xpool + slot * (size_t)j++ - a;
+        if ((rc = mvx_type_unpack(P->dtype, srcs[q], (void *)usrc[q], (size_t)n, st))) return rc;
+        ufold[q] = NULL;
+        if (fold[q]) {
+            ufold[q] = c->xpool + slot * (size_t)j++ - a;
+            if ((rc = mvx_type_unpack(P->dtype, fold[q], (void *)ufold[q], (size_t)n, st))) return rc;
+        }
+    }
+    out = c->xpool + slot * (size_t)j++ - a;
+    if (Q.opkind != MVX_OPKIND_PREDEFINED) {
+        rc = combine_user(c, &Q, usrc, ufold, out, st, a, (size_t)(b - a));
+    } else if (Q.k > MVX_COMBINE_KMAX) {
+        scratch_t S;
+        S.base = c->xpool + slot * (size_t)j - a;
+        S.slot = slot; S.used = 0; S.cap = wide;
+        rc = combine_wide(&Q, usrc, ufold, out, &S, st);
+    } else {
+        unsigned tm, cm;
+        mvx_plan_masks(&Q, &tm, &cm);
+        rc = mvx_op_program(Q.op, Q.dtype, usrc, ufold, Q.k, tm, cm, out, (size_t)n, st);
+    }
+    if (rc) return rc;
+    return mvx_type_pack(P->dtype, out, dst, (size_t)n, st);
+}
+
 static int combine(mvx_comm_t *c, const mvx_plan *P, const char *const *leafp, void *dst,
                    scratch_t *S, hipStream_t st)
 {
@@ -710,7 +842,9 @@ static int combine(mvx_comm_t *c, const mvx_plan *P, const char *const *leafp, v
         srcs[q] = leafp[P->leaf[q]];
         fold[q] = P->leaf_fold[q] >= 0 ? leafp[P->leaf_fold[q]] : NULL;
     }
-    if (P->opkind != MVX_OPKIND_PREDEFINED) return combine_user(c, P, srcs, fold, dst, st);
+    if (P->packed) return combine_packed(c, P, srcs, fold, dst, st);
+    if (P->opkind != MVX_OPKIND_PREDEFINED)
+        return combine_user(c, P, srcs, fold, dst, st, 0, (size_t)(P->c_cnt * P->esize));
     if (P->k > MVX_COMBINE_KMAX) return combine_wide(P, srcs, fold, dst, S, st);
     mvx_plan_masks(P, &tm, &cm);
     return mvx_op_program(P->op, P->dtype, srcs, fold, P->k, tm, cm, dst, (size_t)P->c_cnt, st);
@@ -815,12 +949,8 @@ typedef struct {
 } rank_exec_t;
 
 /* staging layout: one slot per received shard, plus the temporary result
- * of a non-root Reduce; returns the bytes this rank needs.  Consecutive
- * slots are 4 KiB apart beyond their size: back-to-back equal-size shards put
- * the same chunk of every leaf at the same DRAM interleave position, and the
- * k-leaf combine then ran 5-6 % slower (tools/tune_combine_layout.py,
- * profiles/r01/tune_combine_layout.jsonl: 53.9 vs 51.2 us for 8 x 32 MiB). */
-#define SLOT_STAGGER 4096
+ * of a non-root Reduce; returns the bytes this rank needs (slots are
+ * SLOT_STAGGER apart beyond their size). */
 static size_t exec_layout(rank_exec_t *X)
 {
     const mvx_plan *P = X->P;
@@ -1014,7 +1144,6 @@ typedef struct {
     mvx_xport *t;                    /* nr transports */
 } job_t;
 
-static size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 /* every local rank's staging region for plans Q: X[r].P / c set, per-rank
  * offsets in off[], total bytes returned (pool not touched) */
@@ -1384,9 +1513,133 @@ static int run_staged(mvx_comm_t *c, const job_t *J, hipStream_t st)
     return hipStreamSynchronize(st) == hipSuccess ? MPI_SUCCESS : MPI_ERR_OTHER;
 }
 
+/* ---- datatypes with holes: the job on packed copies ----------------------
+ * Each rank's send vector is packed on the device (from an HBM mirror of
+ * its extent-layout region when it is host memory), the plans run on the
+ * packed bytes (what the reference's MPI_Sendrecv moves), and the packed
+ * result is unpacked into recvbuf: type-map bytes only -- a host recvbuf is
+ * mirrored in first so its other bytes come back unchanged. */
+typedef struct { long ext, size, lo, hi; } tspan_t;
+
+static int type_span(int dt, tspan_t *T)
+{
+    if (mvx_type_describe(dt, NULL, NULL, &T->ext, &T->size) ||
+        mvx_type_layout(dt, NULL, NULL, NULL, NULL, &T->lo, &T->hi))
+        return MPI_ERR_TYPE;
+    return MPI_SUCCESS;
+}
+
+/* bytes from origin + lo covering the type maps of n elements */
+static size_t span_bytes(const tspan_t *T, long n)
+{
+    return n > 0 ? (size_t)((n - 1) * T->ext + (T->hi - T->lo)) : 0;
+}
+
+typedef struct {
+    const char *sorg[MVX_MAXP];   /* device origins of the send vectors */
+    char *rorg[MVX_MAXP];         /* device origins of the recv vectors */
+    char *smir[MVX_MAXP], *rmir[MVX_MAXP], *psend[MVX_MAXP], *precv[MVX_MAXP];
+} packed_bufs_t;
+
+static int packed_setup(mvx_comm_t *c, const job_t *J, const tspan_t *T, packed_bufs_t *B, hipStream_t st)
+{
+    const int dt = J->P[0].dtype;
+    size_t need = 0, off[4 * MVX_MAXP];
+    int r, rc;
+    for (r = 0; r < J->nr; r++) {
+        const int sh = J->nsend[r] > 0 && !is_device_ptr(J->send[r]);
+        const int rh = J->nrecv[r] > 0 && !is_device_ptr(J->recv[r]);
+        off[4 * r] = need;     need = al256(need + (sh ? span_bytes(T, J->nsend[r]) : 0));
+        off[4 * r + 1] = need; need = al256(need + (size_t)(J->nsend[r] * T->size));
+        off[4 * r + 2] = need; need = al256(need + (rh ? span_bytes(T, J->nrecv[r]) : 0));
+        off[4 * r + 3] = need; need = al256(need + (size_t)(J->nrecv[r] * T->size));
+        B->smir[r] = sh ? (char *)1 : NULL;
+        B->rmir[r] = rh ? (char *)1 : NULL;
+    }
+    if ((rc = grow(&c->hpool, &c->hpool_bytes, need + 256))) return rc;
+    for (r = 0; r < J->nr; r++) {
+        B->psend[r] = c->hpool + off[4 * r + 1];
+        B->precv[r] = c->hpool + off[4 * r + 3];
+        B->sorg[r] = J->send[r];
+        B->rorg[r] = J->recv[r];
+        if (B->smir[r]) {
+            B->smir[r] = c->hpool + off[4 * r];
+            if (hipMemcpyAsync(B->smir[r], J->send[r] + T->lo, span_bytes(T, J->nsend[r]), hipMemcpyHostToDevice,
+                               st) != hipSuccess)
+                return MPI_ERR_OTHER;
+            B->sorg[r] = B->smir[r] - T->lo;
+        }
+        if (B->rmir[r]) {
+            B->rmir[r] = c->hpool + off[4 * r + 2];
+            if (hipMemcpyAsync(B->rmir[r], J->recv[r] + T->lo, span_bytes(T, J->nrecv[r]), hipMemcpyHostToDevice,
+                               st) != hipSuccess)
+                return MPI_ERR_OTHER;
+            B->rorg[r] = B->rmir[r] - T->lo;
+        }
+        if (J->nsend[r] > 0 && (rc = mvx_type_pack(dt, B->sorg[r], B->psend[r], (size_t)J->nsend[r], st)))
+            return rc;
+    }
+    return MPI_SUCCESS;
+}
+
+static int packed_finish(const job_t *J, const tspan_t *T, packed_bufs_t *B, hipStream_t st, int sync)
+{
+    const int dt = J->P[0].dtype;
+    int r, rc;
+    for (r = 0; r < J->nr; r++) {
+        if (J->nrecv[r] <= 0) continue;
+        if ((rc = mvx_type_unpack(dt, B->precv[r], B->rorg[r], (size_t)J->nrecv[r], st))) return rc;
+        if (B->rmir[r] && hipMemcpyAsync(J->recv[r] + T->lo, B->rmir[r], span_bytes(T, J->nrecv[r]),
+                                         hipMemcpyDeviceToHost, st) != hipSuccess)
+            return MPI_ERR_OTHER;
+    }
+    return (sync && hipStreamSynchronize(st) != hipSuccess) ? MPI_ERR_OTHER : MPI_SUCCESS;
+}
+
+static int run_device(mvx_comm_t *c, const job_t *J, hipStream_t st);
+
+static int run_job_packed(mvx_comm_t *c, const job_t *J, hipStream_t st, int blocking)
+{
+    static job_t K;
+    static packed_bufs_t B;
+    tspan_t T;
+    int r, rc, host = 0;
+    if ((rc = type_span(J->P[0].dtype, &T))) return rc;
+    for (r = 0; r < J->nr; r++)
+        host |= (J->nsend[r] > 0 && !is_device_ptr(J->send[r])) || (J->nrecv[r] > 0 && !is_device_ptr(J->recv[r]));
+    if (host && !blocking) return MPI_ERR_BUFFER;
+    if ((rc = packed_setup(c, J, &T, &B, st))) return rc;
+    K = *J;
+    for (r = 0; r < J->nr; r++) {
+        K.send[r] = B.psend[r];
+        K.recv[r] = B.precv[r];
+    }
+    if ((rc = run_device(c, &K, st))) return rc;
+    return packed_finish(J, &T, &B, st, blocking || host);
+}
+
+/* recvbuf = sendbuf over the type map (MPIR_intra_Scan's self copy when its
+ * op is undefined, intra_scan.c:100-106): through the packed form */
+static int typed_copy(mvx_comm_t *c, int dt, long n, const char *send, char *recv, hipStream_t st, int sync)
+{
+    static job_t K;
+    static packed_bufs_t B;
+    static mvx_plan P0;
+    tspan_t T;
+    int rc;
+    memset(&P0, 0, sizeof P0);
+    P0.dtype = dt;
+    K.nr = 1; K.P = &P0; K.send[0] = send; K.recv[0] = recv; K.nsend[0] = n; K.nrecv[0] = n;
+    if ((rc = type_span(dt, &T)) || (rc = packed_setup(c, &K, &T, &B, st))) return rc;
+    if (n > 0 && hipMemcpyAsync(B.precv[0], B.psend[0], (size_t)(n * T.size), hipMemcpyDeviceToDevice, st) != hipSuccess)
+        return MPI_ERR_OTHER;
+    return packed_finish(&K, &T, &B, st, sync || B.smir[0] || B.rmir[0]);
+}
+
 static int run_job(mvx_comm_t *c, const job_t *J, hipStream_t st, int blocking)
 {
     int r, host = 0, rc;
+    if (J->P[0].packed) return run_job_packed(c, J, st, blocking);
     for (r = 0; r < J->nr; r++)
         host |= (J->nsend[r] > 0 && !is_device_ptr(J->send[r])) ||
                 (J->nrecv[r] > 0 && !is_device_ptr(J->recv[r]));
@@ -1445,6 +1698,7 @@ static int run(mvx_comm_t *c, const call_t *k, hipStream_t st, int blocking)
     if (verdict == MVX_ERR_OP_NOT_DEFINED && k->coll == MVX_COLL_SCAN) {
         /* MPIR_intra_Scan ignores MPIR_Op_errno: recvbuf keeps the self copy
          * (intra_scan.c:100-106) and the call succeeds */
+        if (P.packed) return typed_copy(c, k->dt, nsend, k->sendbuf, k->recvbuf, st, blocking);
         if (hipMemcpyAsync(k->recvbuf, k->sendbuf, (size_t)(nsend * e), hipMemcpyDefault, st) != hipSuccess)
             return MPI_ERR_OTHER;
         return (blocking && hipStreamSynchronize(st) != hipSuccess) ? MPI_ERR_OTHER : MPI_SUCCESS;
@@ -1686,9 +1940,14 @@ static int run_multi(mvx_comm_t *c, int coll, void *const *sendbufs,
     if (verdict) {
         for (r = 0; r < p; r++) {
             rcs[r] = (verdict == MVX_ERR_OP_NOT_DEFINED && !plans[r].calls_uop) ? 0 : verdict;
-            if (coll == MVX_COLL_SCAN && verdict == MVX_ERR_OP_NOT_DEFINED &&
-                hipMemcpyAsync(recvbufs[r], sendbufs[r], (size_t)(count * e), hipMemcpyDefault, st) != hipSuccess)
-                return MPI_ERR_OTHER;
+            if (coll == MVX_COLL_SCAN && verdict == MVX_ERR_OP_NOT_DEFINED && count > 0) {
+                if (plans[r].packed) {
+                    if ((rc = typed_copy(c, dt, count, sendbufs[r], recvbufs[r], st, 1))) return rc;
+                } else if (hipMemcpyAsync(recvbufs[r], sendbufs[r], (size_t)(count * e), hipMemcpyDefault, st) !=
+                           hipSuccess) {
+                    return MPI_ERR_OTHER;
+                }
+            }
         }
         return MPI_SUCCESS;
     }
@@ -1707,6 +1966,7 @@ static int run_multi(mvx_comm_t *c, int coll, void *const *sendbufs,
         t[r].start = lb_nop; t[r].end = lb_nop; t[r].send = lb_send; t[r].recv = lb_recv;
         t[r].lb = &lb; t[r].me = r;
     }
+    if (plans[0].packed) return run_job_packed(c, &J, st, host);
     return host ? run_staged(c, &J, st) : run_device(c, &J, st);
 }
 

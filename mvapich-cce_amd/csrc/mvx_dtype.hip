@@ -1,0 +1,626 @@
+// mvx_dtype.hip -- the datatype engine of the reduction path (libmvx_hip.so).
+//
+// The reference's reductions take any datatype: MPI_Sendrecv moves the type
+// map between ranks (pack on send, unpack into tmp buffers laid out by
+// extent, intra_fns_new.c:5505-5512), and the op sees count elements at the
+// type's extent.  This file keeps a handle table of derived types with the
+// reference's bounds (lb / ub / extent / size, exactly as src/pt2pt computes
+// them, markers and struct alignment included), the flattened type map of
+// each, and the device pack / unpack kernels the executor moves non-dense
+// types with.
+//
+//   MPI_Type_contiguous  type_contig.c:52-187
+//   MPI_Type_vector      type_vec.c:44-110 (-> hvector, or contiguous)
+//   MPI_Type_hvector     type_hvec.c:55-175
+//   MPI_Type_indexed     type_ind.c:74-134 (-> hindexed)
+//   MPI_Type_hindexed    type_hind.c:57-200
+//   MPI_Type_struct      type_struct.c:106-330 (ALIGNMENT_VALUE 0: the x86-64
+//                        "largest member" struct layout, util/structlayout.c)
+//   MPI_Type_commit      type_commit.c:41-143 (dense structs become is_contig)
+//   MPI_Type_free        type_free.c:60-105
+// Basic and pair handles are as MPIR_Init_dtes registers them
+// (initdte.c:106-280, MPIR_Setup_base_datatype 281-310).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <vector>
+
+#include "mvx_mpi.h"
+#include "mvx_hip.h"
+#include "mvx_dtype.h"
+
+namespace mvx {
+namespace dt {
+
+struct Blk { long off, len; };
+
+struct Type {
+    int used, kind, old, count, is_contig, has_lb, has_ub, no_old;
+    long align, extent, size, lb, ub, real_lb, real_ub;
+    // STRUCT members (type_commit's contiguity test)
+    std::vector<long> indices;
+    std::vector<int> blocklens, types;
+    std::vector<Blk> map;       // one element's type map, in order, merged
+    int dense;
+    // the map on the device, split into pieces of <= 64 bytes
+    void *dmap;
+    long dmap_n;
+};
+
+static Type g_t[MVX_TYPE_DERIVED_MAX];
+static const long kMaxBlocks = 1L << 24;
+
+static Type *slot(int h)
+{
+    const int i = h - MVX_TYPE_DERIVED_BASE;
+    if (i < 0 || i >= MVX_TYPE_DERIVED_MAX || !g_t[i].used) return nullptr;
+    return &g_t[i];
+}
+
+static void reset(Type &t)
+{
+    if (t.dmap) (void)hipFree(t.dmap);
+    t = Type();
+}
+
+// The basic and pair handles (initdte.c): fills a view, false if unknown.
+static bool basic(int h, Type &t)
+{
+    t = Type();
+    t.kind = K_BASIC;
+    t.old = h;
+    t.count = 1;
+    t.is_contig = 1;
+    t.dense = 1;
+    auto base = [&](long s) { t.extent = t.size = t.ub = s; t.align = s; t.map.push_back({0, s}); };
+    // the pair structs: {value, int loc} with an MPI_UB at sizeof (initdte.c:169-222)
+    auto pair = [&](long vs, long loc_off, long ext, long al, int contig) {
+        t.extent = t.ub = ext; t.size = vs + 4; t.align = al; t.has_ub = 1; t.is_contig = contig;
+        if (loc_off == vs) t.map.push_back({0, vs + 4});
+        else { t.map.push_back({0, vs}); t.map.push_back({loc_off, 4}); }
+    };
+    switch (h) {
+    case MPI_CHAR: case MPI_UNSIGNED_CHAR: case MPI_BYTE: case MPI_PACKED: base(1); return true;
+    case MPI_SHORT: case MPI_UNSIGNED_SHORT: base(2); return true;
+    case MPI_INT: case MPI_UNSIGNED: case MPI_FLOAT: base(4); return true;
+    case MPI_LONG: case MPI_UNSIGNED_LONG: case MPI_DOUBLE: case MPI_LONG_LONG_INT: base(8); return true;
+    case MPI_LONG_DOUBLE: base(16); return true;
+    case MPI_COMPLEX: base(8); t.align = 4; return true;
+    case MPI_DOUBLE_COMPLEX: base(16); t.align = 8; return true;
+    case MPI_2INT: base(8); t.align = 4; t.old = MPI_INT; t.count = 2; return true;   // contig(2, INT), :167
+    case MPI_FLOAT_INT: pair(4, 4, 8, 4, 1); return true;
+    case MPI_DOUBLE_INT: pair(8, 8, 16, 8, 0); return true;
+    case MPI_LONG_INT: pair(8, 8, 16, 8, 0); return true;
+    case MPI_SHORT_INT: pair(2, 4, 8, 4, 0); return true;
+    case MPI_LONG_DOUBLE_INT: pair(16, 16, 32, 16, 0); return true;
+    case MPI_UB: t.kind = K_UB; t.old = h; return true;     // size 0 (MPIR_Setup_base_datatype)
+    case MPI_LB: t.kind = K_LB; t.old = h; return true;
+    default: return false;
+    }
+}
+
+// a handle's record: the stored derived type, or a view of a basic one
+static const Type *get(int h, Type &view)
+{
+    if (const Type *t = slot(h)) return t;
+    return basic(h, view) ? &view : nullptr;
+}
+
+// append `n` copies of old's map at `base + j * old.extent`
+static bool add_copies(std::vector<Blk> &m, const Type &old, long base, long n)
+{
+    if ((long)m.size() + n * (long)old.map.size() > kMaxBlocks) return false;
+    for (long j = 0; j < n; ++j)
+        for (const Blk &b : old.map) {
+            const long off = base + j * old.extent + b.off;
+            if (!m.empty() && m.back().off + m.back().len == off) m.back().len += b.len;
+            else m.push_back({off, b.len});
+        }
+    return true;
+}
+
+// dense: one element is `extent` whole bytes from its origin (lb 0); the
+// basic pair structs count as whole elements (their padding travels, as
+// the plain path has always moved them)
+static int is_dense(const Type &t)
+{
+    if (t.lb != 0) return 0;
+    if (t.map.size() == 1 && t.map[0].off == 0 && t.map[0].len == t.extent) return 1;
+    return 0;
+}
+
+static int store(Type &n, int *newtype)
+{
+    for (int i = 0; i < MVX_TYPE_DERIVED_MAX; ++i) {
+        if (g_t[i].used) continue;
+        n.used = 1;
+        g_t[i] = n;
+        *newtype = MVX_TYPE_DERIVED_BASE + i;
+        return MPI_SUCCESS;
+    }
+    return MPI_ERR_INTERN;
+}
+
+// type_contig.c:52-187
+static int contiguous(int count, int oldtype, int *newtype)
+{
+    Type ov, iv;
+    if (!newtype) return MPI_ERR_ARG;
+    const Type *o = get(oldtype, ov);
+    if (!o) return MVX_ERR_TYPE_NULL;                               // 66-67
+    if (o->kind == K_UB || o->kind == K_LB) return count < 0 ? MPI_ERR_COUNT : MPI_ERR_TYPE;   // 69-71
+    if (count < 0) return MPI_ERR_COUNT;
+    Type n = Type();
+    n.kind = K_CONTIG;
+    if (count == 0) {                                              // 82-116: empty type
+        n.old = oldtype; n.count = 0; n.is_contig = 1; n.align = 4;
+        n.dense = 1;
+        return store(n, newtype);
+    }
+    // 139-146: a contiguous old type that has an old type itself (MPI_2INT,
+    // a derived contiguous type) is flattened to that old type
+    const bool has_old = oldtype == MPI_2INT || (slot(oldtype) && o->kind == K_CONTIG && !o->no_old);
+    const Type *ot = o;
+    if (o->is_contig && has_old) {
+        ot = get(o->old, iv);
+        n.old = o->old;
+        n.count = count * o->count;
+        n.is_contig = 1;
+    } else {
+        n.old = oldtype;
+        n.count = count;
+        n.is_contig = o->is_contig;
+    }
+    n.align = o->align;
+    n.lb = ot->lb;                                                 // 149-150
+    n.has_lb = ot->has_lb;
+    n.extent = (long)n.count * ot->extent;                         // 151
+    if (ot->has_ub) { n.ub = ot->ub + (long)(count - 1) * ot->extent; n.has_ub = 1; }   // 160-164
+    else n.ub = n.lb + n.extent;
+    n.size = (long)n.count * ot->size;                             // 169
+    n.real_lb = ot->real_lb;
+    n.real_ub = (long)n.count * (ot->real_ub - ot->real_lb) + ot->real_lb;
+    if (!add_copies(n.map, *ot, 0, n.count)) return MPI_ERR_INTERN;
+    n.dense = (ot->dense && n.lb == 0 && ot->lb == 0) ? 1 : is_dense(n);
+    return store(n, newtype);
+}
+
+static int old_checks(const Type *o, int count)
+{
+    if (!o) return MVX_ERR_TYPE_NULL;                   // MPIR_TEST_DTYPE
+    if (count < 0) return MPI_ERR_COUNT;
+    return MPI_SUCCESS;
+}
+
+// type_hvec.c:55-175
+static int hvector(int count, int blocklen, long stride, int oldtype, int *newtype)
+{
+    Type ov;
+    const Type *o = get(oldtype, ov);
+    int rc = old_checks(o, count);
+    if (rc) return rc;
+    if (blocklen < 0) return MPI_ERR_ARG;
+    if (o->kind == K_UB || o->kind == K_LB) return MPI_ERR_TYPE;
+    if ((long)count * blocklen == 0) return contiguous(0, MPI_INT, newtype);     // 87-90
+    if ((long)blocklen * o->extent == stride || count == 1)                      // 93-97
+        return contiguous(count * blocklen, oldtype, newtype);
+    Type n = Type();
+    n.kind = K_HVECTOR;
+    n.old = oldtype;
+    n.count = count;
+    n.align = o->align;
+    n.has_ub = o->has_ub;
+    n.has_lb = o->has_lb;
+    if (o->has_ub) n.ub = stride > 0 ? o->ub + (long)(count - 1) * stride + (long)(blocklen - 1) * o->extent : o->ub;
+    if (o->has_lb) n.lb = stride < 0 ? o->lb + (long)(count - 1) * stride + (long)(blocklen - 1) * o->extent : o->lb;
+    n.extent = (long)(count - 1) * stride + (long)blocklen * o->extent;          // 136
+    if (n.extent < 0) {
+        if (!o->has_ub) n.ub = o->lb;
+        if (!o->has_lb) n.lb = n.ub + n.extent;
+        n.real_ub = o->real_lb;
+        n.real_lb = n.real_ub + (long)(count - 1) * stride + (long)blocklen * (o->real_ub - o->real_lb);
+    } else {
+        if (!o->has_lb) n.lb = o->lb;
+        if (!o->has_ub) n.ub = n.lb + n.extent;
+        n.real_lb = o->real_lb;
+        n.real_ub = n.real_lb + (long)(count - 1) * stride + (long)blocklen * (o->real_ub - o->real_lb);
+    }
+    n.extent = n.ub - n.lb;                                                      // 158
+    n.size = (long)count * blocklen * o->size;
+    for (long i = 0; i < count; ++i)
+        if (!add_copies(n.map, *o, i * stride, blocklen)) return MPI_ERR_INTERN;
+    n.dense = is_dense(n);
+    return store(n, newtype);
+}
+
+// type_vec.c:44-110
+static int vector(int count, int blocklen, int stride, int oldtype, int *newtype)
+{
+    Type ov;
+    const Type *o = get(oldtype, ov);
+    int rc = old_checks(o, count);
+    if (rc) return rc;
+    if (blocklen < 0) return MPI_ERR_ARG;
+    if (o->kind == K_UB || o->kind == K_LB) return MPI_ERR_TYPE;
+    if (blocklen == stride || count == 1) return contiguous(count * blocklen, oldtype, newtype);
+    return hvector(count, blocklen, (long)stride * o->extent, oldtype, newtype);
+}
+
+// type_hind.c:57-200
+static int hindexed(int count, const int *blocklens, const long *indices, int oldtype, int *newtype)
+{
+    Type ov;
+    const Type *o = get(oldtype, ov);
+    int rc = old_checks(o, count);
+    if (rc) return rc;
+    if (o->kind == K_UB || o->kind == K_LB) return MPI_ERR_TYPE;
+    long total = 0;
+    for (int i = 0; i < count; ++i) {
+        if (blocklens[i] < 0) return MPI_ERR_ARG;                                // 95-99
+        total += blocklens[i];
+    }
+    if (total == 0) return contiguous(0, MPI_INT, newtype);
+    Type n = Type();
+    n.kind = K_HINDEXED;
+    n.old = oldtype;
+    n.count = count;
+    n.align = o->align;
+    n.has_ub = o->has_ub;
+    n.has_lb = o->has_lb;
+    long low = indices[0], high = indices[0] + (long)blocklens[0] * o->extent;
+    long real_lb = indices[0], real_ub = real_lb, ub_marker = 0, lb_marker = 0;
+    int ub_found = 0, lb_found = 0;
+    for (int i = 0; i < count; ++i) {                                            // 136-170
+        const long ub = indices[i] + (long)blocklens[i] * o->extent, lb = indices[i];
+        if (ub > lb) { if (high < ub) high = ub; if (low > lb) low = lb; }
+        else { if (high < lb) high = lb; if (low > ub) low = ub; }
+        if (indices[i] < real_lb) real_lb = indices[i];
+        if (indices[i] + (long)blocklens[i] * (o->real_ub - o->real_lb) > real_ub)
+            real_ub = indices[i] + (long)blocklens[i] * (o->real_ub - o->real_lb);
+        if (o->has_ub) {
+            const long t = o->ub + indices[i] + (long)(blocklens[i] - 1) * o->extent;
+            if (!ub_found || ub_marker < t) ub_marker = t;
+            ub_found = 1;
+        }
+        if (o->has_lb) {
+            const long t = o->lb + indices[i];
+            if (!lb_found || lb_marker > t) lb_marker = t;
+            lb_found = 1;
+        }
+    }
+    if (o->real_lb != 0) {                                                       // 173-178
+        low += o->real_lb;
+        high += o->real_lb;
+        real_lb += o->real_lb;
+        real_ub = +o->real_lb;      // the reference's `real_ub =+ ...` (an assignment)
+    }
+    n.lb = o->has_lb ? lb_marker : low;
+    n.ub = o->has_ub ? ub_marker : high;
+    n.extent = n.ub - n.lb;
+    n.size = total * o->size;
+    n.real_lb = real_lb;
+    n.real_ub = real_ub;
+    for (int i = 0; i < count; ++i)
+        if (!add_copies(n.map, *o, indices[i], blocklens[i])) return MPI_ERR_INTERN;
+    n.dense = is_dense(n);
+    return store(n, newtype);
+}
+
+// type_ind.c:74-134: displacements in old extents -> hindexed
+static int indexed(int count, const int *blocklens, const int *indices, int oldtype, int *newtype)
+{
+    Type ov;
+    const Type *o = get(oldtype, ov);
+    int rc = old_checks(o, count);
+    if (rc) return rc;
+    if (o->kind == K_UB || o->kind == K_LB) return MPI_ERR_TYPE;
+    long total = 0;
+    for (int i = 0; i < count; ++i) {
+        total += blocklens[i];
+        if (blocklens[i] < 0) return MVX_SETMSG(MPI_ERR_ARG, MVX_ERR_KIND_ARG_ARRAY_VAL);   // 107-112
+    }
+    if (total == 0) return contiguous(0, MPI_INT, newtype);
+    std::vector<long> h(count > 0 ? count : 1);
+    for (int i = 0; i < count; ++i) h[i] = (long)indices[i] * o->extent;
+    return hindexed(count, blocklens, h.data(), oldtype, newtype);
+}
+
+// type_struct.c:106-330
+static int structure(int count, const int *blocklens, const long *indices, const int *types, int *newtype)
+{
+    if (count < 0) return MVX_SETMSG(MPI_ERR_COUNT, 1);                           // 124-129
+    if (count == 0) return contiguous(0, MPI_INT, newtype);
+    long total = 0;
+    for (int i = 0; i < count; ++i) {                                            // 137-156
+        total += blocklens[i];
+        if (blocklens[i] < 0) return MVX_SETMSG(MPI_ERR_ARG, MVX_ERR_KIND_ARG_ARRAY_VAL);
+        if (types[i] == MPI_DATATYPE_NULL) return MVX_SETMSG(MPI_ERR_TYPE, MVX_ERR_KIND_TYPE_ARRAY_NULL);
+    }
+    if (total == 0) return contiguous(0, MPI_INT, newtype);
+    Type n = Type();
+    n.kind = K_STRUCT;
+    n.count = count;
+    n.align = 1;
+    n.old = types[0];
+    long high = 0, low = 0, real_ub = 0, real_lb = 0, ub_marker = 0, lb_marker = 0;
+    int high_init = 0, low_init = 0, real_init = 0, ub_found = 0, lb_found = 0;
+    for (int i = 0; i < count; ++i) {                                            // 204-297
+        Type ov;
+        const Type *o = get(types[i], ov);
+        if (!o) return MVX_ERR_TYPE_NULL;
+        n.indices.push_back(indices[i]);
+        n.blocklens.push_back(blocklens[i]);
+        n.types.push_back(types[i]);
+        if (n.align < o->align) n.align = o->align;
+        if (o->kind == K_UB) {
+            if (!ub_found || indices[i] > ub_marker) ub_marker = indices[i];
+            ub_found = 1;
+        } else if (o->kind == K_LB) {
+            if (!lb_found || indices[i] < lb_marker) lb_marker = indices[i];
+            lb_found = 1;
+        } else {
+            if (!real_init) { real_init = 1; real_lb = o->real_lb; real_ub = o->real_ub; }
+            else { if (o->real_lb < real_lb) real_lb = o->real_lb; if (o->real_ub > real_ub) real_ub = o->real_ub; }
+            if (o->has_ub) {
+                const long t = o->ub + indices[i] + (long)(blocklens[i] - 1) * o->extent;
+                if (ub_marker < t || !ub_found) ub_marker = t;
+                ub_found = 1;
+            }
+            if (o->has_lb) {
+                if (!lb_found || lb_marker > o->lb + indices[i]) lb_marker = o->lb + indices[i];
+                lb_found = 1;
+            }
+            const long lb = indices[i] + o->lb, ub = lb + (long)blocklens[i] * o->extent;
+            if (!high_init) { high = ub; high_init = 1; } else if (ub > high) high = ub;
+            if (!low_init) { low = lb; low_init = 1; } else if (lb < low) low = lb;
+            if (ub > lb) { if (high < ub) high = ub; if (low > lb) low = lb; }
+            else { if (high < lb) high = lb; if (low > ub) low = ub; }
+            if (!add_copies(n.map, *o, indices[i], blocklens[i])) return MPI_ERR_INTERN;
+        }
+        n.size += (long)blocklens[i] * o->size;
+    }
+    if (lb_found) { n.lb = lb_marker; n.has_lb = 1; } else n.lb = low_init ? low : 0;
+    if (ub_found) { n.ub = ub_marker; n.has_ub = 1; } else n.ub = high_init ? high : 0;
+    n.extent = n.ub - n.lb;
+    n.real_ub = real_ub;
+    n.real_lb = real_lb;
+    if (!lb_found && !ub_found) {                                                // 316-326
+        const long eps = n.extent % n.align;
+        if (eps > 0) { n.ub += n.align - eps; n.extent = n.ub - n.lb; }
+    }
+    n.dense = is_dense(n);
+    return store(n, newtype);
+}
+
+// type_commit.c:55-112: a struct whose members are contiguous and back to
+// back from offset 0, with size == extent, is marked contiguous (and loses
+// its old type, so a later MPI_Type_contiguous does not flatten it)
+static int commit(int h)
+{
+    Type *t = slot(h);
+    Type tmp;
+    if (!t) return basic(h, tmp) ? MPI_SUCCESS : MVX_ERR_TYPE_NULL;
+    if (t->is_contig || t->size != t->extent || t->kind != K_STRUCT) return MPI_SUCCESS;
+    long offset = t->indices[0];
+    int contig = offset == 0;
+    for (int j = 0; contig && j < t->count - 1; ++j) {
+        Type v;
+        const Type *o = get(t->types[j], v);
+        if (!o->is_contig) { contig = 0; break; }
+        if (offset + o->extent * (long)t->blocklens[j] != t->indices[j + 1]) { contig = 0; break; }
+        offset += o->extent * (long)t->blocklens[j];
+    }
+    {
+        Type v;
+        const Type *o = get(t->types[t->count - 1], v);
+        if (!o->is_contig) contig = 0;
+    }
+    if (contig) { t->is_contig = 1; t->no_old = 1; }
+    return MPI_SUCCESS;
+}
+
+bool info(int h, Info *out)
+{
+    Type v;
+    const Type *t = get(h, v);
+    if (!t) return false;
+    out->kind = t->kind;
+    out->old = t->old;
+    out->count = t->count;
+    out->is_contig = t->is_contig;
+    out->dense = t->dense;
+    out->extent = t->extent;
+    out->size = t->size;
+    out->lb = t->lb;
+    out->ub = t->ub;
+    out->span_lo = out->span_hi = 0;
+    if (!t->map.empty()) {
+        long lo = t->map[0].off, hi = t->map[0].off + t->map[0].len;
+        for (const Blk &b : t->map) {
+            if (b.off < lo) lo = b.off;
+            if (b.off + b.len > hi) hi = b.off + b.len;
+        }
+        out->span_lo = lo;
+        out->span_hi = hi;
+    }
+    return true;
+}
+
+// ---- pack / unpack --------------------------------------------------------
+// One work item = one piece (<= 64 bytes) of one element's type map.
+// Consecutive threads take consecutive pieces, so the packed side is
+// written contiguously; each thread copies with the widest access its
+// addresses allow.
+
+struct DBlk { long off, poff; int len, pad; };
+
+template <bool PACK>
+__global__ void __launch_bounds__(256)
+k_pack(const char *__restrict__ src, char *__restrict__ dst, const DBlk *__restrict__ map, long nblk,
+       long count, long extent, long size)
+{
+    const long items = count * nblk;
+    for (long t = (long)blockIdx.x * 256 + threadIdx.x; t < items; t += (long)gridDim.x * 256) {
+        const long i = t / nblk;
+        const DBlk m = map[t - i * nblk];
+        const char *s = PACK ? src + i * extent + m.off : src + i * size + m.poff;
+        char *d = PACK ? dst + i * size + m.poff : dst + i * extent + m.off;
+        const uintptr_t a = (uintptr_t)s | (uintptr_t)d | (uintptr_t)m.len;
+        if ((a & 15) == 0) {
+            for (int b = 0; b < m.len; b += 16) *(uint4 *)(d + b) = *(const uint4 *)(s + b);
+        } else if ((a & 3) == 0) {
+            for (int b = 0; b < m.len; b += 4) *(uint32_t *)(d + b) = *(const uint32_t *)(s + b);
+        } else {
+            for (int b = 0; b < m.len; ++b) d[b] = s[b];
+        }
+    }
+}
+
+static int device_map(Type &t)
+{
+    if (t.dmap) return MPI_SUCCESS;
+    std::vector<DBlk> v;
+    long poff = 0;
+    for (const Blk &b : t.map)
+        for (long o = 0; o < b.len; o += 64) {
+            const long len = b.len - o < 64 ? b.len - o : 64;
+            v.push_back({b.off + o, poff, (int)len, 0});
+            poff += len;
+        }
+    if (v.empty()) return MPI_SUCCESS;
+    if (hipMalloc(&t.dmap, v.size() * sizeof(DBlk)) != hipSuccess) { t.dmap = nullptr; return MPI_ERR_OTHER; }
+    if (hipMemcpy(t.dmap, v.data(), v.size() * sizeof(DBlk), hipMemcpyHostToDevice) != hipSuccess)
+        return MPI_ERR_OTHER;
+    t.dmap_n = (long)v.size();
+    return MPI_SUCCESS;
+}
+
+static int pack(int h, const void *src, void *dst, size_t count, hipStream_t st, bool packing)
+{
+    Type *t = slot(h);
+    Type v;
+    if (!t) {
+        // a basic type is its own packed form
+        if (!basic(h, v)) return MPI_ERR_TYPE;
+        if (!count || !v.size) return MPI_SUCCESS;
+        if (v.map.size() == 1)
+            return hipMemcpyAsync(dst, src, count * (size_t)v.size, hipMemcpyDeviceToDevice, st) == hipSuccess
+                   ? MPI_SUCCESS : MPI_ERR_OTHER;
+        return MPI_ERR_TYPE;   // the padded pair structs move whole (mvx_dtype.h dense)
+    }
+    if (!count || !t->size) return MPI_SUCCESS;
+    int rc = device_map(*t);
+    if (rc) return rc;
+    const long items = (long)count * t->dmap_n;
+    long blocks = (items + 255) / 256;
+    if (blocks > 65536) blocks = 65536;
+    if (packing)
+        hipLaunchKernelGGL(k_pack<true>, dim3((unsigned)blocks), dim3(256), 0, st, (const char *)src, (char *)dst,
+                           (const DBlk *)t->dmap, t->dmap_n, (long)count, t->extent, t->size);
+    else
+        hipLaunchKernelGGL(k_pack<false>, dim3((unsigned)blocks), dim3(256), 0, st, (const char *)src, (char *)dst,
+                           (const DBlk *)t->dmap, t->dmap_n, (long)count, t->extent, t->size);
+    return hipGetLastError() == hipSuccess ? MPI_SUCCESS : MPI_ERR_OTHER;
+}
+
+}  // namespace dt
+}  // namespace mvx
+
+using namespace mvx::dt;
+
+extern "C" int mvx_type_describe(int type, int *oldtype, int *count, long *extent, long *size)
+{
+    Info in;
+    if (!info(type, &in) || in.kind == K_UB || in.kind == K_LB) return MPI_ERR_TYPE;
+    if (oldtype) *oldtype = in.old;
+    if (count) *count = in.count;
+    if (extent) *extent = in.extent;
+    if (size) *size = in.size;
+    return MPI_SUCCESS;
+}
+
+extern "C" int mvx_type_layout(int type, int *kind, int *dense, long *lb, long *ub, long *span_lo,
+                               long *span_hi)
+{
+    Info in;
+    if (!info(type, &in)) return MPI_ERR_TYPE;
+    if (kind) *kind = in.kind;
+    if (dense) *dense = in.dense;
+    if (lb) *lb = in.lb;
+    if (ub) *ub = in.ub;
+    if (span_lo) *span_lo = in.span_lo;
+    if (span_hi) *span_hi = in.span_hi;
+    return MPI_SUCCESS;
+}
+
+extern "C" int mvx_type_contiguous(int count, int oldtype, int *newtype)
+{
+    return contiguous(count, oldtype, newtype);
+}
+
+extern "C" int mvx_type_vector(int count, int blocklen, int stride, int oldtype, int *newtype)
+{
+    if (!newtype) return MPI_ERR_ARG;
+    return vector(count, blocklen, stride, oldtype, newtype);
+}
+
+extern "C" int mvx_type_hvector(int count, int blocklen, long stride, int oldtype, int *newtype)
+{
+    if (!newtype) return MPI_ERR_ARG;
+    return hvector(count, blocklen, stride, oldtype, newtype);
+}
+
+extern "C" int mvx_type_indexed(int count, const int *blocklens, const int *indices, int oldtype,
+                                int *newtype)
+{
+    if (!newtype || (count > 0 && (!blocklens || !indices))) return MPI_ERR_ARG;
+    return indexed(count, blocklens, indices, oldtype, newtype);
+}
+
+extern "C" int mvx_type_hindexed(int count, const int *blocklens, const long *indices, int oldtype,
+                                 int *newtype)
+{
+    if (!newtype || (count > 0 && (!blocklens || !indices))) return MPI_ERR_ARG;
+    return hindexed(count, blocklens, indices, oldtype, newtype);
+}
+
+extern "C" int mvx_type_struct(int count, const int *blocklens, const long *indices, const int *types,
+                               int *newtype)
+{
+    if (!newtype || (count > 0 && (!blocklens || !indices || !types))) return MPI_ERR_ARG;
+    return structure(count, blocklens, indices, types, newtype);
+}
+
+extern "C" int mvx_type_commit(int type) { return commit(type); }
+
+// type_free.c:60-105
+extern "C" int mvx_type_free(int *type)
+{
+    Type v;
+    if (!type) return MPI_ERR_ARG;
+    Type *t = slot(*type);
+    if (!t) {
+        if (*type != MPI_DATATYPE_NULL && basic(*type, v)) return MVX_ERR_PERM_TYPE;
+        return MVX_ERR_TYPE_NULL;
+    }
+    reset(*t);
+    *type = MPI_DATATYPE_NULL;
+    return MPI_SUCCESS;
+}
+
+extern "C" int mvx_dtype_extent(int dtype)
+{
+    long e;
+    return mvx_type_describe(dtype, nullptr, nullptr, &e, nullptr) ? 0 : (int)e;
+}
+
+extern "C" int mvx_type_pack(int type, const void *origin, void *packed, size_t count, void *stream)
+{
+    return pack(type, origin, packed, count, (hipStream_t)stream, true);
+}
+
+extern "C" int mvx_type_unpack(int type, const void *packed, void *origin, size_t count, void *stream)
+{
+    return pack(type, packed, origin, count, (hipStream_t)stream, false);
+}

@@ -34,6 +34,7 @@
 #include "mvx_mpi.h"
 #include "mvx_hip.h"
 #include "mvx_xf80.h"
+#include "mvx_dtype.h"
 
 namespace mvx {
 
@@ -465,53 +466,26 @@ enum { EK_NONE = 0, EK_I8, EK_U8, EK_BYTE, EK_I16, EK_U16, EK_I32, EK_U32,
        // derived contiguous types: count-2 pairs of one base, and the rest
        EK_PP8, EK_PP16, EK_PP64, EK_PPF, EK_PPD, EK_PPX, EK_DERIVED };
 
-// ---------------------------------------------------------------------------
-// derived datatypes (MPI_Type_contiguous, src/pt2pt/type_contig.c:52-187)
-
-struct Derived {
-    int used;
-    int old;         // old type after flattening (a basic or pair handle)
-    int count;       // replication count
-    int is_contig;   // the reference's is_contig (decides later flattening)
-    long extent, size;
-};
-static Derived g_types[MVX_TYPE_DERIVED_MAX];
-
-// the basic and pair handles as MPIR_Init_dtes registers them
-// (initdte.c:106-280): extent, size, is_contig (the pair structs with an
-// MPI_UB past a hole, size != extent, are not contiguous: type_commit.c:67-75)
-static bool basic_info(int dtype, long *e, long *s, int *contig)
+// the op kind of a derived handle (mvx_dtype.hip): MAXLOC / MINLOC are the
+// only ops with derived cases -- a count-2 contiguous type over one base
+// (stride-2 {value, loc} scalars, global_ops.c:1387-1503 / 1625-1740), and an
+// MPIR_STRUCT type by the dte_type of its old_types[0], read as that base's C
+// pair struct (1280-1384 / 1520-1620); every other case is 329
+static int derived_kind(const dt::Info &d)
 {
-    *contig = 1;
-    switch (dtype) {
-    case MPI_CHAR: case MPI_UNSIGNED_CHAR: case MPI_BYTE: case MPI_PACKED: *e = *s = 1; return true;
-    case MPI_SHORT: case MPI_UNSIGNED_SHORT: *e = *s = 2; return true;
-    case MPI_INT: case MPI_UNSIGNED: case MPI_FLOAT: *e = *s = 4; return true;
-    case MPI_LONG: case MPI_UNSIGNED_LONG: case MPI_DOUBLE: case MPI_LONG_LONG_INT: *e = *s = 8; return true;
-    case MPI_LONG_DOUBLE: *e = *s = 16; return true;
-    case MPI_FLOAT_INT: *e = 8; *s = 8; return true;
-    case MPI_2INT: *e = 8; *s = 8; return true;
-    case MPI_DOUBLE_INT: *e = 16; *s = 12; *contig = 0; return true;
-    case MPI_LONG_INT: *e = 16; *s = 12; *contig = 0; return true;
-    case MPI_SHORT_INT: *e = 8; *s = 6; *contig = 0; return true;
-    case MPI_LONG_DOUBLE_INT: *e = 32; *s = 20; *contig = 0; return true;
-    case MPI_COMPLEX: *e = *s = 8; return true;
-    case MPI_DOUBLE_COMPLEX: *e = *s = 16; return true;
-    default: return false;
+    if (d.kind == dt::K_STRUCT) {
+        switch (d.old) {
+        case MPI_INT: return EK_PII;             // MPIR_2int_loctype
+        case MPI_FLOAT: return EK_PFI;
+        case MPI_LONG: case MPI_LONG_LONG_INT: return EK_PLI;
+        case MPI_SHORT: return EK_PSI;
+        case MPI_DOUBLE: return EK_PDI;
+        case MPI_LONG_DOUBLE: return EK_LDBL_INT;
+        default: return EK_DERIVED;
+        }
     }
-}
-
-static Derived *derived(int h)
-{
-    const int i = h - MVX_TYPE_DERIVED_BASE;
-    if (i < 0 || i >= MVX_TYPE_DERIVED_MAX || !g_types[i].used) return nullptr;
-    return &g_types[i];
-}
-
-static int derived_kind(const Derived *d)
-{
-    if (d->count != 2) return EK_DERIVED;
-    switch (d->old) {              // the base's dte_type, global_ops.c:1395-1497
+    if (d.kind != dt::K_CONTIG || d.count != 2) return EK_DERIVED;
+    switch (d.old) {              // the base's dte_type, global_ops.c:1395-1497
     case MPI_INT: return EK_PII;
     case MPI_LONG: case MPI_LONG_LONG_INT: return EK_PP64;
     case MPI_SHORT: return EK_PP16;
@@ -526,8 +500,8 @@ static int derived_kind(const Derived *d)
 static int ekind(int dtype)
 {
     if (dtype >= MVX_TYPE_DERIVED_BASE) {
-        const Derived *d = derived(dtype);
-        return d ? derived_kind(d) : EK_NONE;
+        dt::Info d;
+        return dt::info(dtype, &d) ? derived_kind(d) : EK_NONE;
     }
     switch (dtype) {
     case MPI_CHAR: return EK_I8;
@@ -714,89 +688,11 @@ extern "C" int mvx_op_supported(int op, int dtype)
     return lookup(op, dtype, &rc) != nullptr;
 }
 
-extern "C" int mvx_type_describe(int type, int *oldtype, int *count, long *extent, long *size)
+extern "C" int mvx_op_element_size(int op, int dtype)
 {
-    long e, s;
-    int contig, old = type, cnt = 1;
-    if (const Derived *d = derived(type)) {
-        old = d->old; cnt = d->count; e = d->extent; s = d->size;
-    } else if (basic_info(type, &e, &s, &contig)) {
-        if (type == MPI_2INT) { old = MPI_INT; cnt = 2; }   // initdte.c:167
-    } else {
-        return MPI_ERR_TYPE;
-    }
-    if (oldtype) *oldtype = old;
-    if (count) *count = cnt;
-    if (extent) *extent = e;
-    if (size) *size = s;
-    return MPI_SUCCESS;
-}
-
-// type_contig.c:52-187: argument checks (66-75), then the flattening of a
-// contiguous old type that has an old type itself (139-146), extent and size
-// from the old type (149-169)
-extern "C" int mvx_type_contiguous(int count, int oldtype, int *newtype)
-{
-    Derived o, n;
-    long be, bs;   // extent / size of one element of n.old
-    if (!newtype) return MPI_ERR_ARG;
-    if (oldtype == MPI_LB || oldtype == MPI_UB)       // valid handles, refused (70-71)
-        return count < 0 ? MPI_ERR_COUNT : MPI_ERR_TYPE;
-    if (const Derived *d = derived(oldtype)) {
-        o = *d;
-    } else {
-        int c;
-        memset(&o, 0, sizeof o);
-        if (!basic_info(oldtype, &o.extent, &o.size, &c)) return MVX_ERR_TYPE_NULL;   // 66-67
-        o.is_contig = c;
-        o.old = oldtype == MPI_2INT ? MPI_INT : oldtype;      // MPI_2INT = contig(2, INT)
-        o.count = oldtype == MPI_2INT ? 2 : 1;
-    }
-    const bool has_old = derived(oldtype) || oldtype == MPI_2INT;
-    if (count < 0) return MPI_ERR_COUNT;                        // 69
-    memset(&n, 0, sizeof n);
-    n.used = 1;
-    if (count == 0) {                                           // 82-116: empty type
-        n.old = oldtype; n.count = 0; n.is_contig = 1; be = bs = 0;
-    } else if (o.is_contig && has_old) {                        // 139-142: flatten
-        n.old = o.old; n.count = count * o.count; n.is_contig = 1;
-        be = o.count ? o.extent / o.count : 0;
-        bs = o.count ? o.size / o.count : 0;
-    } else {                                                    // 143-146
-        n.old = oldtype; n.count = count; n.is_contig = o.is_contig;
-        be = o.extent; bs = o.size;
-    }
-    n.extent = (long)n.count * be;                              // 151
-    n.size = (long)n.count * bs;                                // 169
-    for (int i = 0; i < MVX_TYPE_DERIVED_MAX; ++i) {
-        if (g_types[i].used) continue;
-        g_types[i] = n;
-        *newtype = MVX_TYPE_DERIVED_BASE + i;
-        return MPI_SUCCESS;
-    }
-    return MPI_ERR_INTERN;
-}
-
-// type_free.c:60-105
-extern "C" int mvx_type_free(int *type)
-{
-    long e, s;
-    int c;
-    if (!type) return MPI_ERR_ARG;
-    Derived *d = derived(*type);
-    if (!d) {
-        if (*type != MPI_DATATYPE_NULL && basic_info(*type, &e, &s, &c)) return MVX_ERR_PERM_TYPE;
-        return MVX_ERR_TYPE_NULL;
-    }
-    memset(d, 0, sizeof *d);
-    *type = MPI_DATATYPE_NULL;
-    return MPI_SUCCESS;
-}
-
-extern "C" int mvx_dtype_extent(int dtype)
-{
-    long e;
-    return mvx_type_describe(dtype, nullptr, nullptr, &e, nullptr) ? 0 : (int)e;
+    int rc;
+    const KSet *ks = lookup(op, dtype, &rc);
+    return ks ? ks->esize : 0;
 }
 
 extern "C" int mvx_op_apply(int op, int dtype, const void *in, void *inout,

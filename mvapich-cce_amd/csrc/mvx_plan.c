@@ -289,6 +289,11 @@ static int plan_body(mvx_plan *P, int coll, int p, int rank, long count,
     for (i = 0; i < MVX_MAXK; i++) P->leaf_fold[i] = -1;
     P->coll = coll; P->p = p; P->rank = rank; P->root = root;
     P->op = op; P->dtype = dtype; P->esize = e;
+    {   /* a type map with holes moves packed: MPI_Type_size bytes per element */
+        int dense = 1;
+        mvx_type_layout(dtype, NULL, &dense, NULL, NULL, NULL, NULL);
+        if (!dense) { P->packed = 1; P->esize = ts; }
+    }
     P->symmetric = kind == MVX_OPKIND_PREDEFINED && op_symmetric(op, dtype);
     P->opkind = kind;
     P->shape = MVX_SHAPE_TREE;

@@ -84,14 +84,11 @@ static int commute(int op) { return permanent(op) ? 1 : g_uops[op - 200].commute
  * semantics: padding of the destination is left alone) */
 static void tm_copy(void *dst, const void *src, long n, int dtype)
 {
-    int e, s, old, cnt;
+    int e, s;
     long i;
+    if (orc_type_copy(dst, src, n, dtype) == 0) return;   /* derived: its type map */
     orc_dtype_info(dtype, &e, &s);
     if (e == s) { memcpy(dst, src, (size_t)(n * e)); return; }
-    if (orc_type_parts(dtype, &old, &cnt) == 0) {   /* derived over a padded type */
-        tm_copy(dst, src, n * cnt, old);
-        return;
-    }
     for (i = 0; i < n; i++) {
         char *d = (char *)dst + i * e;
         const char *x = (const char *)src + i * e;

@@ -45,86 +45,20 @@ typedef struct { long v; int l; } p_long_int;     /* initdte.c:86-90 */
 typedef struct { short v; int l; } p_short_int;   /* initdte.c:92-96 */
 typedef struct { long double v; int l; } p_ldouble_int;
 
-/* ---------------------------------------------------------------------- */
-/* Derived contiguous types, restating src/pt2pt/type_contig.c:52-187: a
- * contiguous old type that has an old type itself (MPI_2INT = contig(2, INT),
- * or a derived contiguous type) is flattened (139-146); extent and size are
- * count times the old type's (151, 169).  Handles 256 + slot. */
-#define DT_BASE 256
-#define DT_MAX 256
-static struct { int used, old, count, is_contig; long extent, size; } g_dt[DT_MAX];
-
-static int dt_slot(int h)
+/* Derived types live in cpu_types.c (handles 256 + slot). */
+static int is_derived(int h)
 {
-    int i = h - DT_BASE;
-    return (i >= 0 && i < DT_MAX && g_dt[i].used) ? i : -1;
-}
-
-static int basic_contig(int dtype)   /* structs with a hole are not contiguous */
-{
-    return !(dtype == T_DOUBLE_INT || dtype == T_LONG_INT || dtype == T_SHORT_INT ||
-             dtype == T_LDOUBLE_INT);
-}
-
-int orc_type_parts(int dtype, int *old, int *count)
-{
-    int i = dt_slot(dtype);
-    if (i < 0) return ERR_TYPE;
-    *old = g_dt[i].old;
-    *count = g_dt[i].count;
-    return 0;
-}
-
-int orc_type_contiguous(int count, int oldtype, int *newtype)
-{
-    int e, s, i, has_old, o_contig, o_old, o_count, n_old, n_count, n_contig;
-    long be, bs, o_ext, o_size;
-    if (oldtype == T_LB || oldtype == T_UB) return count < 0 ? 2 : ERR_TYPE;
-    if ((i = dt_slot(oldtype)) >= 0) {
-        o_contig = g_dt[i].is_contig; o_old = g_dt[i].old; o_count = g_dt[i].count;
-        o_ext = g_dt[i].extent; o_size = g_dt[i].size; has_old = 1;
-    } else {
-        if (orc_dtype_info(oldtype, &e, &s)) return 3 | (5 << 6);
-        o_contig = basic_contig(oldtype); o_ext = e; o_size = s;
-        has_old = oldtype == T_2INT;
-        o_old = has_old ? T_INT : oldtype; o_count = has_old ? 2 : 1;
-    }
-    if (count < 0) return 2;
-    if (count == 0) {
-        n_old = oldtype; n_count = 0; n_contig = 1; be = bs = 0;
-    } else if (o_contig && has_old) {
-        n_old = o_old; n_count = count * o_count; n_contig = 1;
-        be = o_count ? o_ext / o_count : 0; bs = o_count ? o_size / o_count : 0;
-    } else {
-        n_old = oldtype; n_count = count; n_contig = o_contig; be = o_ext; bs = o_size;
-    }
-    for (i = 0; i < DT_MAX; i++) {
-        if (g_dt[i].used) continue;
-        g_dt[i].used = 1; g_dt[i].old = n_old; g_dt[i].count = n_count;
-        g_dt[i].is_contig = n_contig;
-        g_dt[i].extent = (long)n_count * be; g_dt[i].size = (long)n_count * bs;
-        *newtype = DT_BASE + i;
-        return 0;
-    }
-    return 16;
-}
-
-int orc_type_free(int *dtype)
-{
-    int i = dt_slot(*dtype);
-    if (i < 0) return 3 | (5 << 6);
-    memset(&g_dt[i], 0, sizeof g_dt[i]);
-    *dtype = 0;
-    return 0;
+    return orc_derived_info(h, NULL, NULL, NULL, NULL, NULL) == 0;
 }
 
 int orc_dtype_info(int dtype, int *extent, int *type_size)
 {
     int e, s;
-    if (dt_slot(dtype) >= 0) {
-        int i = dt_slot(dtype);
-        if (extent) *extent = (int)g_dt[i].extent;
-        if (type_size) *type_size = (int)g_dt[i].size;
+    if (is_derived(dtype)) {
+        long de, ds;
+        orc_derived_info(dtype, NULL, NULL, NULL, &de, &ds);
+        if (extent) *extent = (int)de;
+        if (type_size) *type_size = (int)ds;
         return 0;
     }
     switch (dtype) {
@@ -248,8 +182,22 @@ static int loc_op(int is_min, int dtype, const void *in, void *inout, int len)
 
 static int derived_loc_op(int is_min, int dtype, const void *in, void *inout, int len)
 {
-    int old, count, i, n2;
-    if (orc_type_parts(dtype, &old, &count) || count != 2) return ERR_OP_NOT_DEFINED;
+    int old, count, i, n2, kind;
+    orc_derived_info(dtype, &kind, &old, &count, NULL, NULL);
+    if (kind == 4) {
+        /* MPIR_STRUCT: the C pair struct of old_types[0]'s dte_type
+         * (global_ops.c:1280-1384, 1520-1620) */
+        switch (old) {
+        case T_INT: return loc_op(is_min, T_2INT, in, inout, len);    /* MPIR_2int_loctype */
+        case T_FLOAT: return loc_op(is_min, T_FLOAT_INT, in, inout, len);
+        case T_LONG: case T_LLONG: return loc_op(is_min, T_LONG_INT, in, inout, len);
+        case T_SHORT: return loc_op(is_min, T_SHORT_INT, in, inout, len);
+        case T_DOUBLE: return loc_op(is_min, T_DOUBLE_INT, in, inout, len);
+        case T_LDOUBLE: return loc_op(is_min, T_LDOUBLE_INT, in, inout, len);
+        default: return ERR_OP_NOT_DEFINED;
+        }
+    }
+    if (kind != 1 || count != 2) return ERR_OP_NOT_DEFINED;
     n2 = len * count;
     switch (old) {
     case T_INT:     CONTIG2_LOOP(int); return 0;
@@ -267,7 +215,7 @@ static int derived_loc_op(int is_min, int dtype, const void *in, void *inout, in
 int orc_op(int op, int dtype, const void *in, void *inout, int len)
 {
     int i;
-    if (dt_slot(dtype) >= 0) {
+    if (is_derived(dtype)) {
         if (op < 100 || op > 111) return ERR_OP;
         if (op == 111 || op == 110) return derived_loc_op(op == 110, dtype, in, inout, len);
         return ERR_OP_NOT_DEFINED;   /* no MPIR_CONTIG case in any other op */

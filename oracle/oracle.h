@@ -38,12 +38,27 @@ extern "C" {
  * map, excluding padding), or MPI_ERR_TYPE (3) for an unregistered handle. */
 int orc_dtype_info(int dtype, int *extent, int *type_size);
 
-/* MPI_Type_contiguous (type_contig.c:52-187) and MPI_Type_free: derived
- * handles 256.. usable everywhere a datatype is; orc_type_parts gives the
- * flattened old type and count.  Codes as the reference (0, 2, 3, 323). */
+/* Derived types (cpu_types.c): the reference's constructors, bounds and
+ * type maps; handles 256.. usable everywhere a datatype is.  Codes as the
+ * reference (0, 2, 3, 12, 16, 323); a negative code -(class | kind << 6) is
+ * one the reference makes with MPIR_Err_setmsg. */
 int orc_type_contiguous(int count, int oldtype, int *newtype);
+int orc_type_vector(int count, int blocklen, int stride, int oldtype, int *newtype);
+int orc_type_hvector(int count, int blocklen, long stride, int oldtype, int *newtype);
+int orc_type_indexed(int count, const int *blocklens, const int *indices, int oldtype, int *newtype);
+int orc_type_hindexed(int count, const int *blocklens, const long *indices, int oldtype, int *newtype);
+int orc_type_struct(int count, const int *blocklens, const long *indices, const int *types, int *newtype);
+int orc_type_commit(int dtype);
 int orc_type_free(int *dtype);
+int orc_type_bounds(int dtype, long *lb, long *ub, long *extent, long *size);
+/* kind: 1 contig, 2 hvector, 3 hindexed, 4 struct; old: the flattened old
+ * type (contig), the old type, or old_types[0] (struct) */
+int orc_derived_info(int dtype, int *kind, int *old, int *count, long *extent, long *size);
 int orc_type_parts(int dtype, int *old, int *count);
+/* n elements, type-map bytes only (what a message moves); 3 if not derived */
+int orc_type_copy(void *dst, const void *src, long n, int dtype);
+long orc_type_nblocks(int dtype);
+int orc_type_block(int dtype, long i, long *off, long *len);
 
 /* One predefined op: inout[i] = in[i] op inout[i] for i < len.
  * Returns 0, or 329 (MPIR_ERR_OP_NOT_DEFINED) for an undefined (op, type)

@@ -51,6 +51,15 @@ def lib():
         L.orc_smp_set.argtypes = [ctypes.c_int] * 7
         L.orc_type_contiguous.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
         L.orc_type_free.argtypes = [ctypes.POINTER(ctypes.c_int)]
+        pint, plong = ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_long)
+        L.orc_type_vector.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, pint]
+        L.orc_type_hvector.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_long, ctypes.c_int, pint]
+        L.orc_type_indexed.argtypes = [ctypes.c_int, pint, pint, ctypes.c_int, pint]
+        L.orc_type_hindexed.argtypes = [ctypes.c_int, pint, plong, ctypes.c_int, pint]
+        L.orc_type_struct.argtypes = [ctypes.c_int, pint, plong, pint, pint]
+        L.orc_type_commit.argtypes = [ctypes.c_int]
+        L.orc_type_bounds.argtypes = [ctypes.c_int, plong, plong, plong, plong]
+        L.orc_type_copy.argtypes = [vp, vp, ctypes.c_long, ctypes.c_int]
         L.orc_threads_coll.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp), ctypes.POINTER(vp),
                                        ctypes.POINTER(vp), ctypes.c_int, ctypes.POINTER(ctypes.c_int),
                                        ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]
@@ -140,6 +149,56 @@ def type_contiguous(count, oldtype):
     h = ctypes.c_int()
     rc = lib().orc_type_contiguous(count, oldtype, ctypes.byref(h))
     return rc, h.value
+
+
+def _ia(vals, ct=ctypes.c_int):
+    return (ct * max(len(vals), 1))(*vals)
+
+
+def type_vector(count, blocklen, stride, oldtype):
+    h = ctypes.c_int()
+    rc = lib().orc_type_vector(count, blocklen, stride, oldtype, ctypes.byref(h))
+    return rc, h.value
+
+
+def type_hvector(count, blocklen, stride, oldtype):
+    h = ctypes.c_int()
+    rc = lib().orc_type_hvector(count, blocklen, stride, oldtype, ctypes.byref(h))
+    return rc, h.value
+
+
+def type_indexed(count, blocklens, indices, oldtype):
+    h = ctypes.c_int()
+    rc = lib().orc_type_indexed(count, _ia(blocklens), _ia(indices), oldtype, ctypes.byref(h))
+    return rc, h.value
+
+
+def type_hindexed(count, blocklens, indices, oldtype):
+    h = ctypes.c_int()
+    rc = lib().orc_type_hindexed(count, _ia(blocklens), _ia(indices, ctypes.c_long), oldtype, ctypes.byref(h))
+    return rc, h.value
+
+
+def type_struct(count, blocklens, indices, types):
+    h = ctypes.c_int()
+    rc = lib().orc_type_struct(count, _ia(blocklens), _ia(indices, ctypes.c_long), _ia(types), ctypes.byref(h))
+    return rc, h.value
+
+
+def type_commit(handle):
+    return lib().orc_type_commit(handle)
+
+
+def type_bounds(handle):
+    """(rc, lb, ub, extent, size)"""
+    v = [ctypes.c_long() for _ in range(4)]
+    rc = lib().orc_type_bounds(handle, *[ctypes.byref(x) for x in v])
+    return (rc,) + tuple(x.value for x in v)
+
+
+def type_copy(dst, src, n, handle):
+    """n elements, type-map bytes only (numpy buffers)."""
+    return lib().orc_type_copy(_ptr(dst), _ptr(src), n, handle)
 
 
 def type_free(handle):

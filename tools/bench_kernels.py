@@ -91,6 +91,15 @@ def main():
     run(mvx, "C3", mvx.MPI_SUM, mvx.MPI_FLOAT, 8, 0, 32 * MIB, 4)
     run(mvx, "C4", mvx.MPI_BAND, mvx.MPI_LONG, 4, 1, 256 * MIB, 2)
     run(mvx, "C5", mvx.MPI_MAXLOC, mvx.MPI_FLOAT_INT, 8, 0, 64 * MIB, 2)
+    if "sweep" in sys.argv[1:]:
+        # edge effects vs steady state: the same programs at other sizes, and
+        # the plain op at the C3 / C5 launch sizes
+        for mib in (32, 96, 512):
+            run(mvx, "C2-%dMiB" % mib, mvx.MPI_SUM, mvx.MPI_FLOAT, 2, 1, mib * MIB, 4 if mib < 512 else 2)
+        for mib in (16, 64, 128, 256):
+            run(mvx, "C3-leaf%dMiB" % mib, mvx.MPI_SUM, mvx.MPI_FLOAT, 8, 0, mib * MIB, 4 if mib <= 64 else 2)
+        for mib in (32, 128, 256):
+            run(mvx, "C5-leaf%dMiB" % mib, mvx.MPI_MAXLOC, mvx.MPI_FLOAT_INT, 8, 0, mib * MIB, 4 if mib <= 64 else 2)
     if "x87" in sys.argv[1:]:
         # x87 long double (integer emulation): apply and the C3 / C5 shapes
         run(mvx, "X2-sum", mvx.MPI_SUM, mvx.MPI_LONG_DOUBLE, 2, 1, 256 * MIB, 4)
