@@ -135,6 +135,12 @@ int MPI_Type_ub(MPI_Datatype datatype, MPI_Aint *displacement);
 typedef int (MVX_Device_function)(const void *invec, void *inoutvec, size_t len,
                                   MPI_Datatype datatype, void *stream);
 int mvx_op_create_device(MVX_Device_function *function, int commute, MPI_Op *op);
+/* MPI_Op_create / MPI_Op_free under names that cannot collide with a host
+ * MPI library's (libmvx_embed.so exports only mvx_* names) */
+int mvx_op_create(MPI_User_function *function, int commute, MPI_Op *op);
+int mvx_op_free(MPI_Op *op);
+/* GPUs visible to this process */
+int mvx_device_count(void);
 int MPI_Error_class(int errorcode, int *errorclass);
 
 /* The same three calls under names that cannot collide with a host MPI

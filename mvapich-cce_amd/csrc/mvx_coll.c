@@ -435,6 +435,11 @@ int MPI_Op_create(MPI_User_function *function, int commute, MPI_Op *op)
     return op_register(function, NULL, commute, op);
 }
 
+int mvx_op_create(MPI_User_function *function, int commute, MPI_Op *op)
+{
+    return op_register(function, NULL, commute, op);
+}
+
 int mvx_op_create_device(MVX_Device_function *function, int commute, MPI_Op *op)
 {
     if (!function) return MPI_ERR_ARG;
@@ -533,6 +538,15 @@ static int op_kind(MPI_Op op)
     const mvx_op_t *o = predefined(op) ? NULL : user_op(op);
     if (!o) return MVX_OPKIND_PREDEFINED;
     return o->commute ? MVX_OPKIND_USER_COMMUTE : MVX_OPKIND_USER_NONCOMMUTE;
+}
+
+int mvx_op_free(MPI_Op *op) { return MPI_Op_free(op); }
+
+int mvx_device_count(void)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) { (void)hipGetLastError(); return 0; }
+    return n;
 }
 
 int MPI_Op_free(MPI_Op *op)  /* opfree.c:51-82 */

@@ -294,7 +294,12 @@ __device__ __forceinline__ void st_chunk(u32x4 *base, long c, const Chunk<T> &x)
     for (int w = 0; w < CG<T>::w; ++w) st<NT>(base + c * CG<T>::w + w, r[w]);
 }
 
-template <int O, typename T, int KMAX, int U, int NT>
+// PROG = 0: the program comes from the masks (any chain of trees over
+// k <= KMAX leaves); PROG = 1: the full balanced tree over exactly KMAX
+// leaves, steps fixed at compile time -- the Allreduce / Reduce order at
+// p = 4 and 8 (Rabenseifner), where the generic form evaluated and
+// discarded 24 masked steps for the 7 the tree needs.
+template <int O, typename T, int KMAX, int U, int NT, int PROG = 0>
 __global__ void __launch_bounds__(256)
 k_combine(const Params P)
 {
@@ -334,7 +339,7 @@ k_combine(const Params P)
             if (c < P.nvec) {
 #pragma unroll
                 for (int q = 0; q < KMAX; ++q)
-                    if (q < k) x[u][q] = ld_chunk<T, NT>(src[q], c);
+                    if (PROG == 1 || q < k) x[u][q] = ld_chunk<T, NT>(src[q], c);
             }
         }
 #pragma unroll
@@ -361,6 +366,15 @@ k_combine(const Params P)
 #pragma unroll
                     for (int j = 0; j < V; ++j) x[u][0].e[j] = F<O, T>::f(x[u][0].e[j], x[u][1].e[j]);
             }
+        } else if constexpr (PROG == 1) {
+#pragma unroll
+            for (int h = 1; h < KMAX; h <<= 1)
+#pragma unroll
+                for (int q = 0; q + h < KMAX; q += 2 * h)
+#pragma unroll
+                    for (int u = 0; u < U; ++u)
+#pragma unroll
+                        for (int j = 0; j < V; ++j) x[u][q].e[j] = F<O, T>::f(x[u][q].e[j], x[u][q + h].e[j]);
         } else {
 #pragma unroll
             for (int l = 0; (1 << l) < KMAX; ++l) {
@@ -405,7 +419,7 @@ typedef void (*KFn)(const Params);
 // The launched template as rocprofv3 names it ("k_combine<2, float, 2, 4,
 // 1>"), from the compiler's own spelling of the template arguments, so
 // profiles and PMC summaries can be matched to what actually ran.
-template <int O, typename T, int KMAX, int U, int NT>
+template <int O, typename T, int KMAX, int U, int NT, int PROG = 0>
 static const char *ksym()
 {
     static char buf[160];
@@ -413,10 +427,12 @@ static const char *ksym()
         const char *pf = __PRETTY_FUNCTION__;
         const char *t = strstr(pf, "T = ");
         const char *e = t ? strstr(t, ", KMAX") : nullptr;
-        if (t && e)
-            snprintf(buf, sizeof buf, "k_combine<%d, %.*s, %d, %d, %d>", O, (int)(e - t - 4), t + 4, KMAX, U, NT);
+        const int tl = (t && e) ? (int)(e - t - 4) : 1;
+        const char *tn = (t && e) ? t + 4 : "?";
+        if (PROG)
+            snprintf(buf, sizeof buf, "k_combine<%d, %.*s, %d, %d, %d, %d>", O, tl, tn, KMAX, U, NT, PROG);
         else
-            snprintf(buf, sizeof buf, "k_combine<%d, ?, %d, %d, %d>", O, KMAX, U, NT);
+            snprintf(buf, sizeof buf, "k_combine<%d, %.*s, %d, %d, %d>", O, tl, tn, KMAX, U, NT);
     }
     return buf;
 }
@@ -428,6 +444,10 @@ struct KSet {
     const void *prog[2];   // KMAX 8 combine program
     SymFn apply_sym[2], prog_sym[2];
     int prog_unroll;       // its chunks in flight per lane
+    const void *prog2[2];  // 4-byte types: the U = 2 program (MVX_PROG_U=2)
+    SymFn prog2_sym[2];
+    const void *tree8[2], *tree4[2];   // PROG = 1: full trees over 8 / 4 leaves
+    SymFn tree8_sym[2], tree4_sym[2];
     int esize;
     int chunk;             // bytes per chunk (16, or the element if wider)
     const char *name;
@@ -441,17 +461,34 @@ static KSet kset(const char *name)
     s.apply[1] = (const void *)&k_combine<O, T, 2, 4, 1>;
     s.apply_sym[0] = &ksym<O, T, 2, 4, 0>;
     s.apply_sym[1] = &ksym<O, T, 2, 4, 1>;
-    // chunks in flight per lane, measured (tools/bench_kernels.py, A/B in one
-    // box): 4-byte elements 2 (config-3 tree 52.4 vs 53.0 us), 8-byte
-    // elements 1 (config-4 chain 217 vs 234 us, config-5 MAXLOC 102 vs
-    // 113 us); 1- and 2-byte elements unpack to 16 or 8 values per chunk and
-    // spill to scratch at 2
-    constexpr int UP = sizeof(T) == 4 ? 2 : 1;
-    s.prog[0] = (const void *)&k_combine<O, T, MVX_COMBINE_KMAX, UP, 0>;
-    s.prog[1] = (const void *)&k_combine<O, T, MVX_COMBINE_KMAX, UP, 1>;
-    s.prog_sym[0] = &ksym<O, T, MVX_COMBINE_KMAX, UP, 0>;
-    s.prog_sym[1] = &ksym<O, T, MVX_COMBINE_KMAX, UP, 1>;
-    s.prog_unroll = UP;
+    // chunks in flight per lane for the k-leaf programs: 1 (round 2,
+    // tools/tune_prog.hip, profiles/r02/tune_prog{32,64}.jsonl: the 8-leaf
+    // f32 tree at 32 / 64 MiB leaves ran 49.2 / 96.9 us at U = 1 against
+    // 50.3 / 101.3 us at U = 2 -- with 8 leaves, one chunk per leaf per lane
+    // is already 8 x 16 bytes in flight); 4-byte types keep a U = 2 build
+    // for A/B runs (MVX_PROG_U=2)
+    s.prog[0] = (const void *)&k_combine<O, T, MVX_COMBINE_KMAX, 1, 0>;
+    s.prog[1] = (const void *)&k_combine<O, T, MVX_COMBINE_KMAX, 1, 1>;
+    s.prog_sym[0] = &ksym<O, T, MVX_COMBINE_KMAX, 1, 0>;
+    s.prog_sym[1] = &ksym<O, T, MVX_COMBINE_KMAX, 1, 1>;
+    s.prog_unroll = 1;
+    s.tree8[0] = (const void *)&k_combine<O, T, 8, 1, 0, 1>;
+    s.tree8[1] = (const void *)&k_combine<O, T, 8, 1, 1, 1>;
+    s.tree8_sym[0] = &ksym<O, T, 8, 1, 0, 1>;
+    s.tree8_sym[1] = &ksym<O, T, 8, 1, 1, 1>;
+    s.tree4[0] = (const void *)&k_combine<O, T, 4, 1, 0, 1>;
+    s.tree4[1] = (const void *)&k_combine<O, T, 4, 1, 1, 1>;
+    s.tree4_sym[0] = &ksym<O, T, 4, 1, 0, 1>;
+    s.tree4_sym[1] = &ksym<O, T, 4, 1, 1, 1>;
+    if constexpr (sizeof(T) == 4) {
+        s.prog2[0] = (const void *)&k_combine<O, T, MVX_COMBINE_KMAX, 2, 0>;
+        s.prog2[1] = (const void *)&k_combine<O, T, MVX_COMBINE_KMAX, 2, 1>;
+        s.prog2_sym[0] = &ksym<O, T, MVX_COMBINE_KMAX, 2, 0>;
+        s.prog2_sym[1] = &ksym<O, T, MVX_COMBINE_KMAX, 2, 1>;
+    } else {
+        s.prog2[0] = s.prog2[1] = nullptr;
+        s.prog2_sym[0] = s.prog2_sym[1] = nullptr;
+    }
 
     s.esize = (int)sizeof(T);
     s.chunk = CG<T>::bytes;
@@ -624,6 +661,8 @@ static int g_block_cap = 1 << 20;
 // Non-temporal above this many bytes touched by one launch (all operands +
 // the result); below it the result is likely re-read from L2 / MALL.
 static long g_nt_min_bytes = 64L << 20;
+static int g_prog_u = 1;
+static int g_generic_only = 0;   // MVX_PROG_GENERIC=1: no fixed-tree kernels (A/B runs)
 static const char *g_last = "";
 static char g_last_buf[96];
 static const char *g_last_sym = "";
@@ -637,6 +676,10 @@ static void init_env()
     if (e) g_nt_min_bytes = atol(e);
     e = getenv("MVX_BLOCK_CAP");
     if (e && atoi(e) > 0) g_block_cap = atoi(e);
+    e = getenv("MVX_PROG_U");
+    if (e && atoi(e) == 2) g_prog_u = 2;
+    e = getenv("MVX_PROG_GENERIC");
+    if (e && atoi(e) == 1) g_generic_only = 1;
 }
 
 static int launch(const KSet *ks, const void *const fns[2], const SymFn syms[2], int unroll,
@@ -742,6 +785,12 @@ extern "C" int mvx_op_program(int op, int dtype, const void *const *srcs,
         if (k == 2 && !(tree_mask & 1u) && !(chain_mask & 2u)) return MPI_ERR_ARG;
         return launch(ks, ks->apply, ks->apply_sym, 4, P, (hipStream_t)stream);
     }
+    init_env();
+    if (!g_generic_only && chain_mask == 0 && (k == 8 || k == 4) && tree_mask == mvx_tree_mask(k))
+        return k == 8 ? launch(ks, ks->tree8, ks->tree8_sym, 1, P, (hipStream_t)stream)
+                      : launch(ks, ks->tree4, ks->tree4_sym, 1, P, (hipStream_t)stream);
+    if (g_prog_u == 2 && ks->prog2[0])
+        return launch(ks, ks->prog2, ks->prog2_sym, 2, P, (hipStream_t)stream);
     return launch(ks, ks->prog, ks->prog_sym, ks->prog_unroll, P, (hipStream_t)stream);
 }
 

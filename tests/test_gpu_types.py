@@ -1,0 +1,187 @@
+"""GPU: derived datatypes with holes on the device path.
+
+* pack / unpack (mvx_type_pack / mvx_type_unpack): unpack(pack(x)) into a
+  patterned buffer equals the oracle's type-map copy (oracle/cpu_types.c)
+  -- type-map bytes moved, every other byte untouched -- for vector,
+  hvector, indexed, hindexed, struct and nested types.
+* collectives: MAXLOC / MINLOC on struct types (by the first member,
+  global_ops.c:1280-1384; {double, int} moves packed, {float, int} whole), a
+  user op on a struct with a hole, and the reference's 329 for other ops, on
+  virtual communicators p = 1..8, device and host buffers, against the
+  oracle's replay -- whole recv buffers compared, so bytes outside the type
+  map must keep the caller's pattern as in the reference.
+"""
+import numpy as np
+import pytest
+
+import mvxtest as T
+import uops
+
+pytestmark = pytest.mark.gpu
+
+I, D, F, C, B = 6, 11, 10, 1, 3
+
+
+def _both(mvx, oracle, ctor, *args):
+    rm, hm = getattr(mvx, "MPI_Type_" + ctor)(*args)
+    ro, ho = getattr(oracle, "type_" + ctor)(*args)
+    assert rm == ro == 0 and hm == ho, (ctor, args, rm, ro)
+    assert mvx.MPI_Type_commit(hm) == 0 and oracle.type_commit(ho) == 0
+    return hm
+
+
+def _types(mvx, oracle):
+    """name -> handle, built identically on both sides (handles agree)."""
+    t = {}
+    t["vec_int"] = _both(mvx, oracle, "vector", 3, 2, 5, I)             # 3 x 2 ints, stride 5
+    t["hvec_dbl"] = _both(mvx, oracle, "hvector", 4, 1, 24, D)          # doubles 24 bytes apart
+    t["idx_int"] = _both(mvx, oracle, "indexed", 3, [2, 1, 3], [0, 4, 7], I)
+    t["hidx_chr"] = _both(mvx, oracle, "hindexed", 3, [3, 1, 2], [1, 9, 13], C)
+    t["st_di"] = _both(mvx, oracle, "struct", 2, [1, 1], [0, 8], [D, I])   # {double; int}: 16 / 12
+    t["st_id"] = _both(mvx, oracle, "struct", 2, [1, 1], [0, 8], [I, D])   # {int; hole; double}
+    t["st_fi"] = _both(mvx, oracle, "struct", 2, [1, 1], [0, 4], [F, I])   # {float; int}: dense
+    t["st_ci"] = _both(mvx, oracle, "struct", 3, [1, 2, 1], [0, 4, 14], [C, I, B])
+    t["nest"] = _both(mvx, oracle, "contiguous", 3, t["vec_int"])
+    t["vec_st"] = _both(mvx, oracle, "vector", 2, 1, 3, t["st_di"])
+    return t
+
+
+@pytest.fixture(scope="module")
+def types(mvx, oracle):
+    t = _types(mvx, oracle)
+    yield t
+    for h in t.values():
+        mvx.MPI_Type_free(h)
+        oracle.type_free(h)
+
+
+def test_pack_unpack_match_the_type_map(mvx, oracle, types):
+    import torch
+    for name, h in types.items():
+        ext = mvx.MPI_Type_extent(h)[1]
+        size = mvx.MPI_Type_size(h)[1]
+        L = mvx.type_layout(h)
+        assert L["span_lo"] >= 0
+        for n in (1, 7, 1000, 65537):
+            nb = (n - 1) * ext + L["span_hi"]
+            rng = np.random.default_rng(n + h)
+            x = rng.integers(0, 256, nb, dtype=np.uint8)
+            y0 = np.full(nb, 0xAB, np.uint8)
+            dx = torch.from_numpy(x).cuda()
+            dp = torch.zeros(max(n * size, 1), dtype=torch.uint8, device="cuda")
+            dy = torch.from_numpy(y0).cuda()
+            assert mvx.type_pack(h, dx, dp, n) == 0
+            assert mvx.type_unpack(h, dp, dy, n) == 0
+            ref = y0.copy()
+            assert oracle.type_copy(ref, x, n, h) == 0
+            assert np.array_equal(T.from_dev(dy), ref), (name, n)
+            if L["dense"]:
+                assert size == ext
+
+
+def _coll(comm, coll, sends, recvs, n, dt, op, root=0, cnts=None):
+    if coll == "ar":
+        return comm.allreduce_multi(sends, recvs, n, dt, op)
+    if coll == "red":
+        return comm.reduce_multi(sends, recvs, n, dt, op, root)
+    if coll == "scan":
+        return comm.scan_multi(sends, recvs, n, dt, op)
+    return comm.reduce_scatter_multi(sends, recvs, cnts, dt, op)
+
+
+def _oracle(oracle, coll, S, R, n, dt, op, root=0, cnts=None):
+    if coll == "ar":
+        return oracle.allreduce(S, R, n, dt, op)
+    if coll == "red":
+        return oracle.reduce(S, R, n, dt, op, root)
+    if coll == "scan":
+        return oracle.scan(S, R, n, dt, op)
+    return oracle.reduce_scatter(S, R, cnts, dt, op)
+
+
+def _pairs_bytes(h, n, ext, seed, kind):
+    """n elements of a struct {value, int loc} laid out by extent, ties
+    included; the bytes outside the type map random too."""
+    rng = np.random.default_rng(seed)
+    b = rng.integers(0, 256, n * ext, dtype=np.uint8)
+    v = b.reshape(n, ext)
+    if kind == "di":
+        vals = rng.integers(-3, 4, n).astype(np.float64)
+        vals[rng.random(n) < 0.05] = np.nan
+        v[:, 0:8] = vals.view(np.uint8).reshape(n, 8)
+        v[:, 8:12] = rng.integers(-9, 9, n).astype(np.int32).view(np.uint8).reshape(n, 4)
+    elif kind == "fi":
+        v[:, 0:4] = rng.integers(-3, 4, n).astype(np.float32).view(np.uint8).reshape(n, 4)
+        v[:, 4:8] = rng.integers(-9, 9, n).astype(np.int32).view(np.uint8).reshape(n, 4)
+    else:   # id: {int a; hole; double b}
+        v[:, 0:4] = rng.integers(-1000, 1000, n).astype(np.int32).view(np.uint8).reshape(n, 4)
+        v[:, 8:16] = (rng.standard_normal(n) * 100).astype(np.float64).view(np.uint8).reshape(n, 8)
+    return b
+
+
+CASES = [("st_di", 111, "di"), ("st_di", 110, "di"), ("st_fi", 111, "fi"), ("st_id", "idsum", "id")]
+
+
+@pytest.mark.parametrize("where", ["device", "host"])
+@pytest.mark.parametrize("p", [1, 2, 3, 4, 8])
+@pytest.mark.parametrize("tname,op,kind", CASES)
+def test_struct_collectives_match_reference(mvx, oracle, types, where, p, tname, op, kind):
+    import torch
+    h = types[tname]
+    ext = mvx.MPI_Type_extent(h)[1]
+    comm = mvx.Comm.local_ranks(p, 0)
+    uop = None
+    if op == "idsum":
+        rc, uop = (mvx.op_create_device(uops.dev_fn("idsum"), 1) if where == "device"
+                   else mvx.MPI_Op_create(uops.host_fn("idsum"), 1))
+        assert rc == 0
+        assert oracle.user_op_set(250, uops.host_fn("idsum"), 1) == 0
+    try:
+        for coll, n in (("ar", 3), ("ar", 70001), ("red", 5000), ("rs", 1500), ("scan", 800)):
+            cnts = [n // p + (r % 2) for r in range(p)] if coll == "rs" else None
+            tot = sum(cnts) if cnts else n
+            S = [_pairs_bytes(h, tot, ext, 17 * p + r + tot, kind) for r in range(p)]
+            nrecv = [(cnts[r] if cnts else tot) for r in range(p)]
+            R0 = [np.full(max(k, 1) * ext, 0x5C, np.uint8) for k in nrecv]      # caller's pattern
+            if where == "device":
+                sends = [torch.from_numpy(s).cuda() for s in S]
+                recvs = [torch.from_numpy(r.copy()).cuda() for r in R0]
+            else:
+                sends = [s.copy() for s in S]
+                recvs = [r.copy() for r in R0]
+            root = p - 1
+            r, rcs = _coll(comm, coll, sends, recvs, tot, h, uop if uop else op, root, cnts)
+            assert r == 0, (coll, n, r)
+            ref = [x.copy() for x in R0]
+            rref = _oracle(oracle, coll, S, ref, tot, h, 250 if uop else op, root, cnts)
+            assert rcs == rref, (coll, n)
+            for q in range(p):
+                got = recvs[q] if isinstance(recvs[q], np.ndarray) else T.from_dev(recvs[q])
+                assert np.array_equal(got, ref[q]), (tname, op, coll, n, q)
+    finally:
+        comm.free()
+        if uop:
+            mvx.MPI_Op_free(uop)
+
+
+def test_undefined_ops_and_refused_layouts(mvx, oracle, types):
+    """329 for SUM on a struct and MAXLOC on a vector (every rank that calls
+    the op); MAXLOC on a struct whose extent is not its first member's pair
+    struct is refused (MPI_ERR_TYPE, a documented deviation: the reference's
+    element-overlapping reads have no reorderable equivalent)."""
+    import torch
+    comm = mvx.Comm.local_ranks(4, 0)
+    x = [torch.zeros(64 * 64, dtype=torch.uint8, device="cuda") for _ in range(4)]
+    y = [torch.zeros(64 * 64, dtype=torch.uint8, device="cuda") for _ in range(4)]
+    for h, op in ((types["st_di"], 102), (types["vec_int"], 111), (types["nest"], 110)):
+        r, rcs = comm.allreduce_multi(x, y, 16, h, op)
+        assert r == 0 and rcs == [329] * 4
+    r, rcs = comm.allreduce_multi(x, y, 16, types["st_ci"], 111)      # CHAR first: 329
+    assert rcs == [329] * 4
+    # {float; int; hole} (extent 12) -> the FLOAT_INT kernel reads 8-byte pairs
+    rm, odd = mvx.MPI_Type_struct(3, [1, 1, 1], [0, 4, 12], [F, I, mvx.MPI_UB])
+    assert rm == 0 and mvx.MPI_Type_extent(odd)[1] == 12
+    r, rcs = comm.allreduce_multi(x, y, 16, odd, 111)
+    assert r == mvx.MPI_ERR_TYPE
+    mvx.MPI_Type_free(odd)
+    comm.free()

@@ -14,6 +14,9 @@
  *   uop_affine  unsigned long: (a, b) in the two 32-bit halves is the map
  *                        x -> a*x + b; the result is in composed after
  *                        inout, which is associative but not commutative
+ *   uop_idsum   struct {int a; (4-byte hole); double b}, a derived struct
+ *                        type: a and b summed field by field, the hole
+ *                        never read or written
  */
 #include <stdint.h>
 
@@ -81,5 +84,18 @@ void uop_affine(void *in, void *inout, int *len, int *dt)
         const uint32_t a2 = (uint32_t)b[i], b2 = (uint32_t)(b[i] >> 32);
         /* x -> a2*(a1*x + b1) + b2 */
         b[i] = (uint64_t)(a1 * a2) | ((uint64_t)(a2 * b1 + b2) << 32);
+    }
+}
+
+typedef struct { int a; int hole; double b; } idpair_t;
+
+void uop_idsum(void *in, void *inout, int *len, int *dt)
+{
+    const idpair_t *x = (const idpair_t *)in;
+    idpair_t *y = (idpair_t *)inout;
+    (void)dt;
+    for (int i = 0; i < *len; i++) {
+        y[i].a = (int)((unsigned)x[i].a + (unsigned)y[i].a);
+        y[i].b = x[i].b + y[i].b;
     }
 }

@@ -48,7 +48,28 @@ int launch(const void *in, void *inout, size_t len, void *stream)
     return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 
+struct IdPair { int a; int hole; double b; };
+
+__global__ void __launch_bounds__(256) k_idsum(const IdPair *x, IdPair *y, size_t n)
+{
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+        y[i].a = (int)((unsigned)x[i].a + (unsigned)y[i].a);
+        y[i].b = x[i].b + y[i].b;
+    }
+}
+
 }  // namespace
+
+extern "C" int duop_idsum(const void *in, void *inout, size_t len, int dt, void *s)
+{
+    (void)dt;
+    if (len == 0) return 0;
+    size_t blocks = (len + 255) / 256;
+    if (blocks > 65536) blocks = 65536;
+    hipLaunchKernelGGL(k_idsum, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)s, (const IdPair *)in,
+                       (IdPair *)inout, len);
+    return hipGetLastError() == hipSuccess ? 0 : 1;
+}
 
 extern "C" int duop_mix(const void *in, void *inout, size_t len, int dt, void *s) { (void)dt; return launch<Mix>(in, inout, len, s); }
 extern "C" int duop_affine(const void *in, void *inout, size_t len, int dt, void *s) { (void)dt; return launch<Affine>(in, inout, len, s); }

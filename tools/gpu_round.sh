@@ -43,11 +43,21 @@ if [[ $STAGE == all || $STAGE == host ]]; then
   run timeout -k 10 300 python tools/bench_host.py "$@" > gpurun_out/bench_host.jsonl 2> gpurun_out/bench_host.err || { tail -20 gpurun_out/bench_host.err; exit 1; }
   cat gpurun_out/bench_host.jsonl
 fi
+if [[ $STAGE == kernels_ab ]]; then
+  # fixed-tree programs (default) against the generic masked program
+  # (MVX_PROG_GENERIC=1), interleaved on one box
+  for r in 1 2; do
+    for g in 0 1; do
+      MVX_PROG_GENERIC=$g run timeout -k 10 300 python tools/bench_kernels.py > gpurun_out/bench_kernels_g${g}_$r.jsonl 2>> gpurun_out/bench_kernels.err || exit 1
+    done
+  done
+  for f in gpurun_out/bench_kernels_g*_*.jsonl; do echo "-- $f"; cut -c1-150 $f; done
+fi
 if [[ $STAGE == pmc_kernels ]]; then
   rm -rf gpurun_out/pmck_f gpurun_out/pmck_w
   run timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmck_f -o f -- python3 tools/bench_kernels.py > gpurun_out/pmck_f.log 2>&1 || exit 1
   run timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmck_w -o w -- python3 tools/bench_kernels.py > gpurun_out/pmck_w.log 2>&1 || exit 1
-  python3 tools/pmc_summary.py gpurun_out/pmck_f gpurun_out/pmck_w "k_combine<2, float, 8, 2, 1>" sum_f32_k8_nt 33554432 301989888 gpurun_out/pmc_c3.json && \
+  python3 tools/pmc_summary.py gpurun_out/pmck_f gpurun_out/pmck_w "k_combine<2, float, 8, 1, 1>" sum_f32_k8_nt 33554432 301989888 gpurun_out/pmc_c3.json && \
   python3 tools/pmc_summary.py gpurun_out/pmck_f gpurun_out/pmck_w "k_combine<5, unsigned long, 8, 1, 1>" band_u64_k4_nt 268435456 1342177280 gpurun_out/pmc_c4.json && \
   python3 tools/pmc_summary.py gpurun_out/pmck_f gpurun_out/pmck_w "k_combine<11, mvx::pfi, 8, 1, 1>" maxloc_float_int_k8_nt 67108864 603979776 gpurun_out/pmc_c5.json
 fi
