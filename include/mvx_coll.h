@@ -23,13 +23,13 @@
 
 #include <stddef.h>
 #include "mvx_mpi.h"
+#include "mvx_embed.h"   /* mvx_tuning, mvx_type_set_handle; shared with libmvx_embed.so */
 
 #ifdef __cplusplus
 extern "C" {
 #endif
 
 /* ---- communicators ----------------------------------------------------- */
-#define MVX_UNIQUE_ID_BYTES 128
 
 /* rank 0 creates the id, every rank passes the same bytes to mvx_comm_init */
 int mvx_get_unique_id(void *id_out);
@@ -254,18 +254,7 @@ int mvx_op_errno(void);
  * (intra_fns_new.c:293-310), whose small-message path is a leader folding the
  * node's ranks in rank order (4992-5198, 5793-5940), with runtime knobs read
  * by MPIR_Init (initutil.c:230-293).  Here the flavour is per communicator. */
-typedef struct mvx_tuning {
-    int smp;                        /* 1: _SMP_ collops, 0: ch_shmem collops  */
-    int enable_shmem_collectives;   /* initutil.c:146; VIADEV_USE_SHMEM_COLL=0,
-                                       VIADEV_USE_BLOCKING=1, (MV|VIADEV)_USE_
-                                       SHARED_MEM=0 clear it                  */
-    int shmem_coll_ok;              /* the comm holds a shmem collective block
-                                       (create_2level_comm.c:199-225, 274-279) */
-    int disable_shmem_reduce;       /* !VIADEV_USE_SHMEM_REDUCE              */
-    int disable_shmem_allreduce;    /* !VIADEV_USE_SHMEM_ALLREDUCE           */
-    int shmem_coll_reduce_threshold;     /* bytes, default 1 << 10 (:70)    */
-    int shmem_coll_allreduce_threshold;  /* bytes, default 1 << 15 (:71)    */
-} mvx_tuning;
+/* typedef struct mvx_tuning: include/mvx_embed.h */
 
 /* The knobs of an `smp` build after MPIR_Init's environment parsing
  * (VIADEV_USE_SHMEM_REDUCE, VIADEV_USE_SHMEM_ALLREDUCE, VIADEV_USE_BLOCKING,

@@ -1,0 +1,78 @@
+/*
+ * mvx_embed.h -- the surface of libmvx_embed.so, the host library built to be
+ * linked INTO an MPI implementation (integration/intra_mvx.c).  It declares
+ * only mvx_* names with plain int handles, so it can be included next to the
+ * host MPI's own mpi.h / mpiimpl.h without redefining MPI_Comm, MPI_SUM ...
+ * (libmvx_embed.so exports nothing else, embed.map).  Every function here is
+ * also in libmvx.so; mvx_coll.h includes this header so the compiler checks
+ * the two declarations agree.
+ *
+ * Handles: datatypes and ops are libmvx's (include/mvx_mpi.h).  The
+ * predefined ones have the reference's values (include/mpi.h:64-140), so a
+ * permanent MPIR_DATATYPE's `self` and a predefined MPI_Op pass unchanged;
+ * derived types are rebuilt with the mvx_type_* constructors of
+ * include/mvx_hip.h and user ops registered with mvx_op_create.
+ */
+#ifndef MVX_EMBED_H
+#define MVX_EMBED_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MVX_UNIQUE_ID_BYTES 128
+
+/* communicators: one process per GPU, collective over `size` processes */
+int mvx_get_unique_id(void *id_out);
+int mvx_comm_init(int *comm, int rank, int size, int device, const void *unique_id);
+int mvx_comm_free(int *comm);
+int mvx_device_count(void);
+/* 1 if p is device (or managed) memory */
+int mvx_buffer_is_device(const void *p);
+
+/* the reduction collectives (reduce.c:62-96, allreduce.c:57-92,
+ * red_scat.c:60-90, scan.c:55-95): same argument checks in the same order,
+ * same return codes; device or host buffers */
+int mvx_coll_reduce(void *sendbuf, void *recvbuf, int count, int datatype, int op, int root,
+                    int comm);
+int mvx_coll_allreduce(void *sendbuf, void *recvbuf, int count, int datatype, int op, int comm);
+int mvx_coll_reduce_scatter(void *sendbuf, void *recvbuf, int *recvcnts, int datatype, int op,
+                            int comm);
+int mvx_coll_scan(void *sendbuf, void *recvbuf, int count, int datatype, int op, int comm);
+
+/* user ops: MPI_User_function with int handles (include/mpi.h:282) */
+typedef void(mvx_user_function)(void *invec, void *inoutvec, int *len, int *datatype);
+int mvx_op_create(mvx_user_function *function, int commute, int *op);
+int mvx_op_free(int *op);
+
+/* The datatype handle a user function receives for libmvx type `type`
+ * (default: `type` itself).  A binding that rebuilds the host MPI's derived
+ * type as a libmvx type sets the host MPI's handle here, so the function
+ * sees the handle its caller passed, as in the reference ((*uop)(..., &type),
+ * intra_fns_new.c:5697).  handle == type removes the mapping.  Returns 0, or
+ * MPI_ERR_OTHER (15) when the table (256 entries) is full. */
+int mvx_type_set_handle(int type, int handle);
+
+/* device flavour and collective knobs (the reference's _SMP_ collops) */
+typedef struct mvx_tuning {
+    int smp;                        /* 1: _SMP_ collops, 0: ch_shmem collops  */
+    int enable_shmem_collectives;   /* initutil.c:146; VIADEV_USE_SHMEM_COLL=0,
+                                       VIADEV_USE_BLOCKING=1, (MV|VIADEV)_USE_
+                                       SHARED_MEM=0 clear it                  */
+    int shmem_coll_ok;              /* the comm holds a shmem collective block
+                                       (create_2level_comm.c:199-225, 274-279) */
+    int disable_shmem_reduce;       /* !VIADEV_USE_SHMEM_REDUCE              */
+    int disable_shmem_allreduce;    /* !VIADEV_USE_SHMEM_ALLREDUCE           */
+    int shmem_coll_reduce_threshold;     /* bytes, default 1 << 10 (:70)    */
+    int shmem_coll_allreduce_threshold;  /* bytes, default 1 << 15 (:71)    */
+} mvx_tuning;
+int mvx_tuning_from_env(mvx_tuning *t, int smp);
+int mvx_comm_get_tuning(int comm, mvx_tuning *t);
+int mvx_comm_set_tuning(int comm, const mvx_tuning *t);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MVX_EMBED_H */

@@ -183,6 +183,7 @@ def _load():
     _hip.mvx_type_unpack.argtypes = [i, vp, vp, sz, vp]
     _hip.mvx_op_element_size.argtypes = [i, i]
     c.MPI_Type_commit.argtypes = [pi]
+    c.mvx_type_set_handle.argtypes = [i, i]
     c.MPI_Type_free.argtypes = [pi]
     c.MPI_Type_extent.argtypes = [i, pl]
     c.MPI_Type_size.argtypes = [i, pi]

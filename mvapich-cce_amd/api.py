@@ -15,7 +15,7 @@ __all__ = [
     "MPIR_call", "op_errno", "last_kernel", "last_kernel_symbol", "set_launch",
     "MPI_Type_contiguous", "MPI_Type_commit", "MPI_Type_free", "MPI_Type_extent", "MPI_Type_size",
     "MPI_Type_vector", "MPI_Type_hvector", "MPI_Type_indexed", "MPI_Type_hindexed", "MPI_Type_struct",
-    "MPI_Type_lb", "MPI_Type_ub", "type_layout", "type_pack", "type_unpack",
+    "MPI_Type_lb", "MPI_Type_ub", "type_layout", "type_set_handle", "type_pack", "type_unpack",
 ]
 
 
@@ -341,6 +341,12 @@ def type_layout(datatype):
     if rc:
         raise ValueError("mvx_type_layout rc=%d" % rc)
     return dict(kind=k.value, dense=d.value, lb=lb.value, ub=ub.value, span_lo=lo.value, span_hi=hi.value)
+
+
+def type_set_handle(datatype, handle):
+    """The handle user functions receive for `datatype` (mvx_type_set_handle,
+    include/mvx_embed.h); handle == datatype removes the mapping."""
+    return coll().mvx_type_set_handle(datatype, handle)
 
 
 def type_pack(datatype, origin, packed, count, stream=None):

@@ -609,12 +609,44 @@ static size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
  * program runs over k scratch copies of the leaves (a user function writes
  * its inout operand, and leaves include the caller's send buffer); a swap
  * just renames which scratch buffer holds the left value. */
+/* the handle a user function is given for a libmvx type (mvx_embed.h) */
+#define MAX_TYPE_ALIASES 256
+static struct { int type, handle; } g_alias[MAX_TYPE_ALIASES];
+static int g_nalias;
+
+int mvx_type_set_handle(int type, int handle)
+{
+    int i;
+    for (i = 0; i < g_nalias; i++)
+        if (g_alias[i].type == type) break;
+    if (handle == type) {
+        if (i < g_nalias) g_alias[i] = g_alias[--g_nalias];
+        return MPI_SUCCESS;
+    }
+    if (i == g_nalias) {
+        if (g_nalias == MAX_TYPE_ALIASES) return MPI_ERR_OTHER;
+        g_nalias++;
+    }
+    g_alias[i].type = type;
+    g_alias[i].handle = handle;
+    return MPI_SUCCESS;
+}
+
+static MPI_Datatype user_handle(MPI_Datatype dt)
+{
+    int i;
+    for (i = 0; i < g_nalias; i++)
+        if (g_alias[i].type == dt) return g_alias[i].handle;
+    return dt;
+}
+
 static int call_host(const mvx_op_t *o, const char *in, char *inout, long n, int esize,
                      MPI_Datatype dt)
 {
+    const MPI_Datatype uh = user_handle(dt);
     while (n > 0) {   /* the reference's len is an int */
         int len = n > 0x40000000L ? 0x40000000 : (int)n;
-        MPI_Datatype t = dt;
+        MPI_Datatype t = uh;
         o->op((void *)in, inout, &len, &t);
         in += (long)len * esize;
         inout += (long)len * esize;
@@ -626,7 +658,7 @@ static int call_host(const mvx_op_t *o, const char *in, char *inout, long n, int
 static int user_step(const mvx_op_t *o, const char *in, char *inout, long n, int esize,
                      MPI_Datatype dt, hipStream_t st)
 {
-    if (o->dop) return o->dop(in, inout, (size_t)n, dt, st) ? MPI_ERR_OTHER : MPI_SUCCESS;
+    if (o->dop) return o->dop(in, inout, (size_t)n, user_handle(dt), st) ? MPI_ERR_OTHER : MPI_SUCCESS;
     return call_host(o, in, inout, n, esize, dt);
 }
 

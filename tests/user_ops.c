@@ -68,9 +68,12 @@ void uop_mix(void *in, void *inout, int *len, int *dt)
 /* uop_mix over a derived type of 3 unsigned words (MPI_Type_contiguous(3,
  * MPI_UNSIGNED)): *len counts derived elements, so 3 * *len words -- the
  * element-wise contract a user function has with its datatype */
+int uop_last_dt;   /* the datatype handle uop_mix3 was last given */
+
 void uop_mix3(void *in, void *inout, int *len, int *dt)
 {
     int n = 3 * *len;
+    uop_last_dt = *dt;
     uop_mix(in, inout, &n, dt);
 }
 
