@@ -226,8 +226,11 @@ def run_single(args, mvx, dev):
 # ------------------------------------------------------------------ common --
 
 def timed(args, step, stream, world):
-    """W untimed steps, then K steps between barrier + synchronize; per-step
-    HIP events on the launch stream give mean / median / min."""
+    """W untimed steps, then K steps between barrier + synchronize, with one
+    HIP event pair on the launch stream around them (the mean: nothing else
+    is enqueued between the steps).  Then, untimed, K more steps with an
+    event after each for the median / min (an event between two kernels adds
+    a few microseconds of its own, so these are not used for the mean)."""
     import torch
     import torch.distributed as dist
 
@@ -239,16 +242,22 @@ def timed(args, step, stream, world):
     for _ in range(args.warmup):
         step()
     barrier()
-    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
+    e0.record(stream)
+    for i in range(args.steps):
+        step()
+    e1.record(stream)
+    barrier()
+    wall = time.perf_counter() - t0
+    dev_ms = e0.elapsed_time(e1)
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     evs[0].record(stream)
     for i in range(args.steps):
         step()
         evs[i + 1].record(stream)
     barrier()
-    wall = time.perf_counter() - t0
     per = [evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)]
-    dev_ms = evs[0].elapsed_time(evs[-1])
     t_local = max(wall, dev_ms / 1e3)
     if world > 1:
         t = torch.tensor([t_local], dtype=torch.float64)

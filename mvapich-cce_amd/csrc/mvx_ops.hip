@@ -429,10 +429,8 @@ static const char *ksym()
         const char *e = t ? strstr(t, ", KMAX") : nullptr;
         const int tl = (t && e) ? (int)(e - t - 4) : 1;
         const char *tn = (t && e) ? t + 4 : "?";
-        if (PROG)
-            snprintf(buf, sizeof buf, "k_combine<%d, %.*s, %d, %d, %d, %d>", O, tl, tn, KMAX, U, NT, PROG);
-        else
-            snprintf(buf, sizeof buf, "k_combine<%d, %.*s, %d, %d, %d>", O, tl, tn, KMAX, U, NT);
+        // every template argument, as rocprofv3 names the kernel
+        snprintf(buf, sizeof buf, "k_combine<%d, %.*s, %d, %d, %d, %d>", O, tl, tn, KMAX, U, NT, PROG);
     }
     return buf;
 }
