@@ -112,21 +112,64 @@ def test_mpir_user_function_symbols(mvx, oracle, name, op):
     assert mvx.op_errno() == 329
 
 
-@pytest.mark.parametrize("n", [1, 1000, 9 * 1024 * 1024 + 5])
-@pytest.mark.parametrize("where", ["host-host", "dev-host", "host-dev"])
+LDI = 22   # MPI_LONG_DOUBLE_INT, 32-byte elements
+
+
+def _place(x, kind):
+    """host (pageable numpy), pin (page-locked torch tensor) or dev"""
+    import torch
+    if kind == "dev":
+        return T.to_dev(x)
+    if kind == "pin":
+        return torch.from_numpy(x.view(np.uint8).copy()).pin_memory()
+    return T.clone(x)
+
+
+def _back(y, kind):
+    if kind == "dev":
+        return T.from_dev(y)
+    if kind == "pin":
+        return y.numpy()
+    return np.asarray(y)
+
+
+@pytest.mark.parametrize("n", [1, 1000, 9 * 1024 * 1024 + 5, 17 * 1024 * 1024 + 3])
+@pytest.mark.parametrize("where", ["host-host", "dev-host", "host-dev", "pin-pin", "pin-host", "host-pin",
+                                   "dev-pin"])
 def test_mpir_host_buffers(mvx, oracle, n, where):
     """MPI user buffers live in host memory: the op streams them through HBM
-    (chunked, H2D / kernel / D2H overlapped) with the same device kernel."""
+    (chunked; pageable operands through pinned bounce slots, page-locked ones
+    DMA'd directly; H2D / kernel / D2H overlapped) with the same kernel."""
     a, b = T.rand_vec(10, n, 5), T.rand_vec(10, n, 6)
     ref = T.clone(b)
     oracle.op(102, 10, a.view(np.uint8), ref.view(np.uint8), n)
-    ia = T.to_dev(a) if where == "dev-host" else a
-    io = T.to_dev(b) if where == "host-dev" else T.clone(b)
+    ki, ko = where.split("-")
+    ia, io = _place(a, ki), _place(b, ko)
     mvx.op_errno()
     mvx.MPIR_call("MPIR_SUM", ia, io, n, mvx.MPI_FLOAT)
     assert mvx.op_errno() == 0
-    got = T.from_dev(io) if where == "host-dev" else io
-    T.assert_same(102, 10, np.asarray(got).view(np.uint8), ref)
+    T.assert_same(102, 10, _back(io, ko).view(np.uint8), ref)
+
+
+@pytest.mark.parametrize("where", ["host-host", "pin-host", "host-pin"])
+@pytest.mark.parametrize("dtype,op", [(13, 109), (18, 111), (12, 100), (8, 105), (LDI, 110)])
+def test_mpir_host_buffers_types(mvx, oracle, where, dtype, op):
+    """Other element sizes (8, 16 and 32-byte elements; the padding of the
+    pair structs is carried from inout) over several chunks, operands offset
+    by one element from their allocation (misaligned against the bounce)."""
+    name = {100: "MPIR_MAXF", 105: "MPIR_BAND", 109: "MPIR_BXOR", 110: "MPIR_MINLOC", 111: "MPIR_MAXLOC"}
+    E = mvx.dtype_info(dtype)[0]
+    n = (80 << 20) // E + 7          # over HOP_BOUNCE_MIN: the bounce pipeline for pageable operands
+    a8 = T.rand_vec(dtype, n + 1, 7).view(np.uint8)[E:]
+    b8 = T.rand_vec(dtype, n + 1, 8).view(np.uint8)[E:]
+    ref = b8.copy()
+    oracle.op(op, dtype, a8.copy(), ref, n)
+    ki, ko = where.split("-")
+    ia, io = _place(a8, ki), _place(b8, ko)
+    mvx.op_errno()
+    mvx.MPIR_call(name[op], ia, io, n, dtype)
+    assert mvx.op_errno() == 0
+    assert np.array_equal(_back(io, ko).view(np.uint8), ref)
 
 
 def test_special_values_float(mvx, oracle):

@@ -17,7 +17,7 @@ PCIe (H2D in, D2H out).  For float32 vectors of 8 B ... 256 MiB, one line per
                 sum of 4 vectors: host buffers staged per rank
 
 Every result is checked against numpy (float32 sums of small integers are
-exact).  usage: bench_host.py [--max-mib 256] [--cases a,b,...]
+exact).  usage: bench_host.py [--min-mib M] [--max-mib 256] [--cases a,b,...]
 """
 import argparse
 import importlib
@@ -49,6 +49,7 @@ def timeit(fn, budget=0.25, max_reps=2000):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--max-mib", type=int, default=256)
+    ap.add_argument("--min-mib", type=int, default=0, help="start the size sweep here (default 8 bytes)")
     ap.add_argument("--cases", default=",".join(ALL))
     args = ap.parse_args()
     cases = args.cases.split(",")
@@ -65,7 +66,7 @@ def main():
     F, SUM = mvx.MPI_FLOAT, mvx.MPI_SUM
 
     sizes = []
-    b = 8
+    b = args.min_mib * MIB if args.min_mib else 8
     while b <= args.max_mib * MIB:
         sizes.append(b)
         b *= 4
