@@ -1188,7 +1188,24 @@ typedef struct {
     char *recv[MVX_MAXP];
     long nsend[MVX_MAXP], nrecv[MVX_MAXP];   /* elements */
     mvx_xport *t;                    /* nr transports */
+    int kinds;                       /* 1: skind / rkind are filled (job_kinds) */
+    int skind[MVX_MAXP], rkind[MVX_MAXP];   /* MVX_BUF_* of send / recv (empty: DEVICE) */
 } job_t;
+
+/* the buffers' kinds, one pointer query each; returns 1 if any is host memory */
+static int job_kinds(job_t *J)
+{
+    int r, host = 0;
+    if (!J->kinds) {
+        for (r = 0; r < J->nr; r++) {
+            J->skind[r] = J->nsend[r] > 0 ? mvx_buf_kind(J->send[r]) : MVX_BUF_DEVICE;
+            J->rkind[r] = J->nrecv[r] > 0 ? mvx_buf_kind(J->recv[r]) : MVX_BUF_DEVICE;
+        }
+        J->kinds = 1;
+    }
+    for (r = 0; r < J->nr; r++) host |= J->skind[r] != MVX_BUF_DEVICE || J->rkind[r] != MVX_BUF_DEVICE;
+    return host;
+}
 
 
 /* every local rank's staging region for plans Q: X[r].P / c set, per-rank
@@ -1416,17 +1433,21 @@ typedef struct {
     int shost[MVX_MAXP], rhost[MVX_MAXP];      /* 1: caller's buffer is host memory */
     int spin[MVX_MAXP], rpin[MVX_MAXP];        /* ... and page-locked */
     long cs;                                   /* slice length, elements */
+    int single;                                /* the job is one slice */
 } stage_job_t;
 
 
-/* slice i in: host -> device for every host send buffer */
+/* slice i in: host -> device for every host send buffer.  A job of one
+ * slice (S->single) copies on the caller's stream itself: nothing to overlap,
+ * and no event round trips on the small-message path. */
 static int stage_in(stage_job_t *S, const mvx_plan *Q, long i, hipStream_t st)
 {
     const int b = (int)(i % STAGE_NB);
+    const hipStream_t hs = S->single ? st : g_stage.sh;
     mvx_range v[MVX_MAXP + 1];
     size_t boff = 0;
     int r, n, j;
-    if (i >= STAGE_NB && hipEventSynchronize(g_stage.ein[b]) != hipSuccess) return MPI_ERR_OTHER;
+    if (!S->single && i >= STAGE_NB && hipEventSynchronize(g_stage.ein[b]) != hipSuccess) return MPI_ERR_OTHER;
     for (r = 0; r < S->J->nr; r++) {
         const long E = Q[r].esize;
         if (!S->shost[r]) continue;
@@ -1439,10 +1460,11 @@ static int stage_in(stage_job_t *S, const mvx_plan *Q, long i, hipStream_t st)
                 src = g_stage.bin[b] + boff;
                 boff += al256(bytes);
             }
-            if (hipMemcpyAsync(S->dsend[r] + o, src, bytes, hipMemcpyHostToDevice, g_stage.sh) != hipSuccess)
+            if (hipMemcpyAsync(S->dsend[r] + o, src, bytes, hipMemcpyHostToDevice, hs) != hipSuccess)
                 return MPI_ERR_OTHER;
         }
     }
+    if (S->single) return MPI_SUCCESS;
     if (hipEventRecord(g_stage.ein[b], g_stage.sh) != hipSuccess ||
         hipStreamWaitEvent(st, g_stage.ein[b], 0) != hipSuccess)
         return MPI_ERR_OTHER;
@@ -1453,11 +1475,12 @@ static int stage_in(stage_job_t *S, const mvx_plan *Q, long i, hipStream_t st)
 static int stage_out(stage_job_t *S, const mvx_plan *Q, long i, hipStream_t st)
 {
     const int b = (int)(i % STAGE_NB);
+    const hipStream_t ds = S->single ? st : g_stage.sd;
     mvx_range v[MVX_MAXP + 1];
     size_t boff = 0;
     int r, n, j;
-    if (hipEventRecord(g_stage.ex[b], st) != hipSuccess ||
-        hipStreamWaitEvent(g_stage.sd, g_stage.ex[b], 0) != hipSuccess)
+    if (!S->single && (hipEventRecord(g_stage.ex[b], st) != hipSuccess ||
+                       hipStreamWaitEvent(g_stage.sd, g_stage.ex[b], 0) != hipSuccess))
         return MPI_ERR_OTHER;
     for (r = 0; r < S->J->nr; r++) {
         const long E = Q[r].esize;
@@ -1467,21 +1490,23 @@ static int stage_out(stage_job_t *S, const mvx_plan *Q, long i, hipStream_t st)
             const size_t o = (size_t)(v[j].off * E), bytes = (size_t)(v[j].cnt * E);
             char *dst = S->rpin[r] ? S->J->recv[r] + o : g_stage.bout[b] + boff;
             if (!S->rpin[r]) boff += al256(bytes);
-            if (hipMemcpyAsync(dst, S->drecv[r] + o, bytes, hipMemcpyDeviceToHost, g_stage.sd) != hipSuccess)
+            if (hipMemcpyAsync(dst, S->drecv[r] + o, bytes, hipMemcpyDeviceToHost, ds) != hipSuccess)
                 return MPI_ERR_OTHER;
         }
     }
+    if (S->single) return MPI_SUCCESS;
     return hipEventRecord(g_stage.eout[b], g_stage.sd) == hipSuccess ? MPI_SUCCESS : MPI_ERR_OTHER;
 }
 
 /* slice i out, finish: wait for its D2H, bounce -> pageable target */
-static int stage_drain(stage_job_t *S, const mvx_plan *Q, long i)
+static int stage_drain(stage_job_t *S, const mvx_plan *Q, long i, hipStream_t st)
 {
     const int b = (int)(i % STAGE_NB);
     mvx_range v[MVX_MAXP + 1];
     size_t boff = 0;
     int r, n, j;
-    if (hipEventSynchronize(g_stage.eout[b]) != hipSuccess) return MPI_ERR_OTHER;
+    if ((S->single ? hipStreamSynchronize(st) : hipEventSynchronize(g_stage.eout[b])) != hipSuccess)
+        return MPI_ERR_OTHER;
     for (r = 0; r < S->J->nr; r++) {
         const long E = Q[r].esize;
         if (!S->rhost[r] || S->rpin[r]) continue;
@@ -1511,10 +1536,10 @@ static int run_staged(mvx_comm_t *c, const job_t *J, hipStream_t st)
     for (r = 0; r < J->nr; r++) {
         const long E = J->P[r].esize;
         int ns = send_ranges(&J->P[r], v), nv = recv_ranges(&J->P[r], v);
-        S.shost[r] = J->nsend[r] > 0 && !is_device_ptr(J->send[r]);
-        S.rhost[r] = J->nrecv[r] > 0 && !is_device_ptr(J->recv[r]);
-        S.spin[r] = S.shost[r] && mvx_host_pinned(J->send[r]);
-        S.rpin[r] = S.rhost[r] && mvx_host_pinned(J->recv[r]);
+        S.shost[r] = J->skind[r] != MVX_BUF_DEVICE;
+        S.rhost[r] = J->rkind[r] != MVX_BUF_DEVICE;
+        S.spin[r] = J->skind[r] == MVX_BUF_PINNED;
+        S.rpin[r] = J->rkind[r] == MVX_BUF_PINNED;
         off[2 * r] = need;
         if (S.shost[r]) need = al256(need + (size_t)(J->nsend[r] * E));
         off[2 * r + 1] = need;
@@ -1544,6 +1569,7 @@ static int run_staged(mvx_comm_t *c, const job_t *J, hipStream_t st)
         if (bounce < 4096) bounce = 4096;
     }
     nsl = span > 0 ? (span + S.cs - 1) / S.cs : 0;
+    S.single = nsl <= 1;
     if ((rc = stage_init(bounce))) return rc;
     for (r = 0; r < J->nr; r++) plan_slice(&J->P[r], 0, S.cs, &g_slice[0][r]);
     if ((rc = job_layout(c, X, J, g_slice[0]))) return rc;   /* slice 0 is the largest */
@@ -1556,9 +1582,9 @@ static int run_staged(mvx_comm_t *c, const job_t *J, hipStream_t st)
         if ((rc = stage_in(&S, Q, i, st))) return rc;
         if ((rc = exec_group(X, J->t, J->nr, st))) return rc;
         if ((rc = stage_out(&S, Q, i, st))) return rc;
-        if (i > 0 && (rc = stage_drain(&S, g_slice[(i - 1) & 1], i - 1))) return rc;
+        if (i > 0 && (rc = stage_drain(&S, g_slice[(i - 1) & 1], i - 1, st))) return rc;
     }
-    if (nsl > 0 && (rc = stage_drain(&S, g_slice[(nsl - 1) & 1], nsl - 1))) return rc;
+    if (nsl > 0 && (rc = stage_drain(&S, g_slice[(nsl - 1) & 1], nsl - 1, st))) return rc;
     return hipStreamSynchronize(st) == hipSuccess ? MPI_SUCCESS : MPI_ERR_OTHER;
 }
 
@@ -1685,14 +1711,11 @@ static int typed_copy(mvx_comm_t *c, int dt, long n, const char *send, char *rec
     return packed_finish(&K, &T, &B, st, sync || B.smir[0] || B.rmir[0]);
 }
 
-static int run_job(mvx_comm_t *c, const job_t *J, hipStream_t st, int blocking)
+static int run_job(mvx_comm_t *c, job_t *J, hipStream_t st, int blocking)
 {
-    int r, host = 0, rc;
+    int rc;
     if (J->P[0].packed) return run_job_packed(c, J, st, blocking);
-    for (r = 0; r < J->nr; r++)
-        host |= (J->nsend[r] > 0 && !is_device_ptr(J->send[r])) ||
-                (J->nrecv[r] > 0 && !is_device_ptr(J->recv[r]));
-    if (host) return blocking ? run_staged(c, J, st) : MPI_ERR_BUFFER;
+    if (job_kinds(J)) return blocking ? run_staged(c, J, st) : MPI_ERR_BUFFER;
     rc = run_device(c, J, st);
     if (rc == MPI_SUCCESS && blocking && hipStreamSynchronize(st) != hipSuccess) rc = MPI_ERR_OTHER;
     return rc;
@@ -1765,6 +1788,7 @@ static int run(mvx_comm_t *c, const call_t *k, hipStream_t st, int blocking)
     }
     t.me = c->rank;
     J.nr = 1;
+    J.kinds = 0;
     J.P = &P;
     J.send[0] = k->sendbuf;
     J.recv[0] = k->recvbuf;
@@ -2010,11 +2034,12 @@ static int run_multi(mvx_comm_t *c, int coll, void *const *sendbufs,
         J.send[r] = (const char *)sendbufs[r];
         J.recv[r] = (char *)recvbufs[r];
         if (J.nsend[r] && J.send[r] == J.recv[r]) return MPI_ERR_BUFFER;
-        host |= (J.nsend[r] > 0 && !is_device_ptr(J.send[r])) || (J.nrecv[r] > 0 && !is_device_ptr(J.recv[r]));
         memset(&t[r], 0, sizeof t[r]);
         t[r].start = lb_nop; t[r].end = lb_nop; t[r].send = lb_send; t[r].recv = lb_recv;
         t[r].lb = &lb; t[r].me = r;
     }
+    J.kinds = 0;
+    host = job_kinds(&J);
     if (plans[0].packed) return run_job_packed(c, &J, st, host);
     return host ? run_staged(c, &J, st) : run_device(c, &J, st);
 }

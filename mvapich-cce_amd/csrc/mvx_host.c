@@ -28,6 +28,18 @@
 
 #include "mvx_internal.h"
 
+int mvx_buf_kind(const void *p)
+{
+    hipPointerAttribute_t a;
+    if (!p) return MVX_BUF_PAGEABLE;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return MVX_BUF_PAGEABLE;
+    }
+    if (a.type == hipMemoryTypeDevice || a.isManaged) return MVX_BUF_DEVICE;
+    return a.type == hipMemoryTypeHost ? MVX_BUF_PINNED : MVX_BUF_PAGEABLE;
+}
+
 int mvx_host_pinned(const void *p)
 {
     hipPointerAttribute_t a;

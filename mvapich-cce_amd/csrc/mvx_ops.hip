@@ -303,6 +303,11 @@ template <int O, typename T, int KMAX, int U, int NT, int PROG = 0>
 __global__ void __launch_bounds__(256)
 k_combine(const Params P)
 {
+    // the launch may reserve dynamic LDS to cap resident blocks per CU
+    // (launch(), g_cap); the kernel never uses it -- the reference here
+    // (never taken) marks the kernel as one that takes dynamic LDS
+    extern __shared__ char lds_cap[];
+    if (P.n < 0) lds_cap[threadIdx.x] = 0;
     constexpr int V = CG<T>::v;
     const long tid = (long)blockIdx.x * 256 + threadIdx.x;
     const long nthr = (long)gridDim.x * 256;
@@ -344,7 +349,10 @@ k_combine(const Params P)
         }
 #pragma unroll
         for (int q = 0; q < KMAX; ++q) {
-            if (q < k && fold[q]) {
+            // fixed trees are launched without folded leaves (mvx_op_program):
+            // no branch between the loads and the tree keeps every load of
+            // the iteration in flight before the first add
+            if (PROG == 0 && q < k && fold[q]) {
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
                     const long c = c0 + (long)u * 256;
@@ -407,6 +415,52 @@ k_combine(const Params P)
     }
 }
 
+// The fixed full tree over the aligned body only: what a large C3 / C5
+// combine is once the plan's blocks are 16-byte aligned and whole (no head,
+// no tail, no folded leaves).  Its prologue is a handful of scalar loads
+// (k_combine's head / tail / misalignment paths are gone), which matters at
+// the few resident blocks per CU the residency cap leaves
+// (tools/tune_occ.hip: the same loop behind k_combine's prologue ran 2 us
+// slower per 50 us launch).
+struct BodyParams {
+    const u32x4 *src[8];
+    u32x4 *dst;
+    long nvec;   // chunks
+};
+
+template <int O, typename T, int KMAX, int U>
+__global__ void __launch_bounds__(256)
+k_tree_body(const BodyParams P)
+{
+    extern __shared__ char lds_cap[];
+    if (P.nvec < 0) lds_cap[threadIdx.x] = 0;
+    constexpr int V = CG<T>::v;
+    const long nthr = (long)gridDim.x * 256;
+    for (long c0 = (long)blockIdx.x * (256 * U) + threadIdx.x; c0 < P.nvec; c0 += nthr * U) {
+        Chunk<T> x[U][KMAX];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const long c = c0 + (long)u * 256;
+            if (c < P.nvec)
+#pragma unroll
+                for (int q = 0; q < KMAX; ++q) x[u][q] = ld_chunk<T, 1>(P.src[q], c);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const long c = c0 + (long)u * 256;
+            if (c < P.nvec) {
+#pragma unroll
+                for (int h = 1; h < KMAX; h <<= 1)
+#pragma unroll
+                    for (int q = 0; q + h < KMAX; q += 2 * h)
+#pragma unroll
+                        for (int j = 0; j < V; ++j) x[u][q].e[j] = F<O, T>::f(x[u][q].e[j], x[u][q + h].e[j]);
+                st_chunk<T, 1>(P.dst, c, x[u][0]);
+            }
+        }
+    }
+}
+
 }  // namespace mvx
 
 // ---------------------------------------------------------------------------
@@ -437,57 +491,89 @@ static const char *ksym()
 
 typedef const char *(*SymFn)();
 
+template <int O, typename T, int KMAX, int U>
+static const char *ksym_body()
+{
+    static char buf[160];
+    if (!buf[0]) {
+        const char *pf = __PRETTY_FUNCTION__;
+        const char *t = strstr(pf, "T = ");
+        const char *e = t ? strstr(t, ", KMAX") : nullptr;
+        const int tl = (t && e) ? (int)(e - t - 4) : 1;
+        const char *tn = (t && e) ? t + 4 : "?";
+        snprintf(buf, sizeof buf, "k_tree_body<%d, %.*s, %d, %d>", O, tl, tn, KMAX, U);
+    }
+    return buf;
+}
+
+// A kernel family: [0] the cached build, [1] the non-temporal one (NT), each
+// with its chunks in flight per lane (U) and its residency class (FAM_*)
+enum { FAM_APPLY = 0, FAM_PROG, FAM_TREE, FAM_N };
+struct KFam {
+    const void *fn[2];
+    SymFn sym[2];
+    int unroll[2];
+    int fam;
+    const void *body;      // FAM_TREE: k_tree_body for large aligned launches, or null
+    SymFn body_sym;
+    int body_unroll;
+};
+
 struct KSet {
-    const void *apply[2];  // KMAX 2 (k <= 2), 4 chunks in flight per lane; [NT]
-    const void *prog[2];   // KMAX 8 combine program
-    SymFn apply_sym[2], prog_sym[2];
-    int prog_unroll;       // its chunks in flight per lane
-    const void *prog2[2];  // 4-byte types: the U = 2 program (MVX_PROG_U=2)
-    SymFn prog2_sym[2];
-    const void *tree8[2], *tree4[2];   // PROG = 1: full trees over 8 / 4 leaves
-    SymFn tree8_sym[2], tree4_sym[2];
+    KFam apply;            // KMAX 2 (k <= 2)
+    KFam prog;             // KMAX 8 combine program (masks)
+    KFam prog2;            // 4-byte types: the U = 2 program (MVX_PROG_U=2); fn[0] null otherwise
+    KFam tree8, tree4;     // PROG = 1: full trees over 8 / 4 leaves
     int esize;
     int chunk;             // bytes per chunk (16, or the element if wider)
     const char *name;
 };
 
+template <int O, typename T, int KMAX, int U0, int U1, int PROG>
+static KFam kfam(int fam)
+{
+    KFam f;
+    f.fn[0] = (const void *)&k_combine<O, T, KMAX, U0, 0, PROG>;
+    f.fn[1] = (const void *)&k_combine<O, T, KMAX, U1, 1, PROG>;
+    f.sym[0] = &ksym<O, T, KMAX, U0, 0, PROG>;
+    f.sym[1] = &ksym<O, T, KMAX, U1, 1, PROG>;
+    f.unroll[0] = U0;
+    f.unroll[1] = U1;
+    f.fam = fam;
+    if constexpr (PROG == 1) {
+        f.body = (const void *)&k_tree_body<O, T, KMAX, U1>;
+        f.body_sym = &ksym_body<O, T, KMAX, U1>;
+        f.body_unroll = U1;
+    } else {
+        f.body = nullptr;
+        f.body_sym = nullptr;
+        f.body_unroll = 0;
+    }
+    return f;
+}
+
+// Chunks in flight per lane, and (launch()) resident blocks per CU, for the
+// non-temporal (large) launches -- round 2, tools/tune_occ.hip,
+// profiles/r02/tune_occ.jsonl: at full occupancy a streaming launch keeps ~10x
+// the bytes in flight Little's law needs and every HBM channel juggles rows
+// from all the streams; fewer resident blocks with more loads each measured
+// k = 8, 8 x 32 MiB: U1 uncapped 76.5 %, U2 at 3 blocks / CU 79.0 %;
+// k = 8, 8 x 64 MiB: 77.0 % -> 79.6 %.  The plain op (k = 2) gains nothing
+// reproducible from a cap and keeps U = 4 at full occupancy, as do the
+// cached (small-launch) builds.
 template <int O, typename T>
 static KSet kset(const char *name)
 {
     KSet s;
-    s.apply[0] = (const void *)&k_combine<O, T, 2, 4, 0>;
-    s.apply[1] = (const void *)&k_combine<O, T, 2, 4, 1>;
-    s.apply_sym[0] = &ksym<O, T, 2, 4, 0>;
-    s.apply_sym[1] = &ksym<O, T, 2, 4, 1>;
-    // chunks in flight per lane for the k-leaf programs: 1 (round 2,
-    // tools/tune_prog.hip, profiles/r02/tune_prog{32,64}.jsonl: the 8-leaf
-    // f32 tree at 32 / 64 MiB leaves ran 49.2 / 96.9 us at U = 1 against
-    // 50.3 / 101.3 us at U = 2 -- with 8 leaves, one chunk per leaf per lane
-    // is already 8 x 16 bytes in flight); 4-byte types keep a U = 2 build
-    // for A/B runs (MVX_PROG_U=2)
-    s.prog[0] = (const void *)&k_combine<O, T, MVX_COMBINE_KMAX, 1, 0>;
-    s.prog[1] = (const void *)&k_combine<O, T, MVX_COMBINE_KMAX, 1, 1>;
-    s.prog_sym[0] = &ksym<O, T, MVX_COMBINE_KMAX, 1, 0>;
-    s.prog_sym[1] = &ksym<O, T, MVX_COMBINE_KMAX, 1, 1>;
-    s.prog_unroll = 1;
-    s.tree8[0] = (const void *)&k_combine<O, T, 8, 1, 0, 1>;
-    s.tree8[1] = (const void *)&k_combine<O, T, 8, 1, 1, 1>;
-    s.tree8_sym[0] = &ksym<O, T, 8, 1, 0, 1>;
-    s.tree8_sym[1] = &ksym<O, T, 8, 1, 1, 1>;
-    s.tree4[0] = (const void *)&k_combine<O, T, 4, 1, 0, 1>;
-    s.tree4[1] = (const void *)&k_combine<O, T, 4, 1, 1, 1>;
-    s.tree4_sym[0] = &ksym<O, T, 4, 1, 0, 1>;
-    s.tree4_sym[1] = &ksym<O, T, 4, 1, 1, 1>;
+    s.apply = kfam<O, T, 2, 4, 4, 0>(FAM_APPLY);
+    s.prog = kfam<O, T, MVX_COMBINE_KMAX, 1, 1, 0>(FAM_PROG);
+    s.tree8 = kfam<O, T, 8, 1, 2, 1>(FAM_TREE);
+    s.tree4 = kfam<O, T, 4, 1, 2, 1>(FAM_TREE);
     if constexpr (sizeof(T) == 4) {
-        s.prog2[0] = (const void *)&k_combine<O, T, MVX_COMBINE_KMAX, 2, 0>;
-        s.prog2[1] = (const void *)&k_combine<O, T, MVX_COMBINE_KMAX, 2, 1>;
-        s.prog2_sym[0] = &ksym<O, T, MVX_COMBINE_KMAX, 2, 0>;
-        s.prog2_sym[1] = &ksym<O, T, MVX_COMBINE_KMAX, 2, 1>;
+        s.prog2 = kfam<O, T, MVX_COMBINE_KMAX, 2, 2, 0>(FAM_PROG);
     } else {
-        s.prog2[0] = s.prog2[1] = nullptr;
-        s.prog2_sym[0] = s.prog2_sym[1] = nullptr;
+        memset(&s.prog2, 0, sizeof s.prog2);
     }
-
     s.esize = (int)sizeof(T);
     s.chunk = CG<T>::bytes;
     s.name = name;
@@ -661,9 +747,16 @@ static int g_block_cap = 1 << 20;
 static long g_nt_min_bytes = 64L << 20;
 static int g_prog_u = 1;
 static int g_generic_only = 0;   // MVX_PROG_GENERIC=1: no fixed-tree kernels (A/B runs)
+// resident blocks per CU for the non-temporal launches of each family (0 =
+// as many as registers allow); MVX_CAP_{APPLY,PROG,TREE} override for A/B runs
+static int g_cap[FAM_N] = {0, 0, 3};
+static int g_no_body = 0;        // MVX_NO_BODY=1: fixed trees through k_combine (A/B runs)
+static size_t g_cap_lds[FAM_N];
 static const char *g_last = "";
 static char g_last_buf[96];
 static const char *g_last_sym = "";
+static unsigned g_last_blocks;
+static size_t g_last_lds;
 
 static void init_env()
 {
@@ -678,16 +771,32 @@ static void init_env()
     if (e && atoi(e) == 2) g_prog_u = 2;
     e = getenv("MVX_PROG_GENERIC");
     if (e && atoi(e) == 1) g_generic_only = 1;
+    e = getenv("MVX_NO_BODY");
+    if (e && atoi(e) == 1) g_no_body = 1;
+    const char *caps[FAM_N] = {"MVX_CAP_APPLY", "MVX_CAP_PROG", "MVX_CAP_TREE"};
+    // gfx950: 160 KiB of LDS per CU (the runtime's per-multiprocessor
+    // attribute reports the 64 KiB per-block limit instead)
+    const int lds_per_cu = 160 * 1024;
+    for (int f = 0; f < FAM_N; ++f) {
+        e = getenv(caps[f]);
+        if (e) g_cap[f] = atoi(e);
+        // dynamic LDS per block that leaves room for g_cap blocks per CU and
+        // not one more (the kernels do not touch it); under 64 KiB needs no
+        // function attribute
+        g_cap_lds[f] = g_cap[f] >= 2 ? ((size_t)lds_per_cu / (size_t)g_cap[f] - 1024) & ~(size_t)1023 : 0;
+        if (g_cap_lds[f] > 64 * 1024) g_cap_lds[f] = 0;
+    }
 }
 
-static int launch(const KSet *ks, const void *const fns[2], const SymFn syms[2], int unroll,
-                  Params &P, hipStream_t stream)
+static int launch(const KSet *ks, const KFam &F, Params &P, hipStream_t stream)
 {
     init_env();
     int nleaves = 0;
     for (int q = 0; q < P.k; ++q) nleaves += 1 + (P.fold[q] != nullptr);
     const int nt = (long)(nleaves + 1) * P.n * ks->esize >= g_nt_min_bytes;
-    const void *fn = fns[nt];
+    const void *fn = F.fn[nt];
+    const int unroll = F.unroll[nt];
+    const size_t lds = nt ? g_cap_lds[F.fam] : 0;
     const int es = ks->esize;
     const uintptr_t m = (uintptr_t)P.dst & 15;
     bool same = true;
@@ -707,15 +816,37 @@ static int launch(const KSet *ks, const void *const fns[2], const SymFn syms[2],
         P.nvec = 0;
         P.vec_ok = 0;
     }
+    bool folded = false;
+    for (int q = 0; q < P.k; ++q) folded |= P.fold[q] != nullptr;
+    if (nt && F.body && !g_no_body && P.vec_ok && P.head == 0 && P.nvec > 0 && P.nvec * ks->chunk == P.n * es &&
+        !folded) {
+        BodyParams B;
+        memset(&B, 0, sizeof B);
+        for (int q = 0; q < P.k; ++q) B.src[q] = reinterpret_cast<const u32x4 *>(P.src[q]);
+        B.dst = reinterpret_cast<u32x4 *>(P.dst);
+        B.nvec = P.nvec;
+        long work = (P.nvec + F.body_unroll * 256 - 1) / (F.body_unroll * 256);
+        const unsigned blocks = (unsigned)(work < g_block_cap ? work : g_block_cap);
+        void *bargs[] = {&B};
+        hipError_t e = hipLaunchKernel(F.body, dim3(blocks), dim3(256), bargs, lds, stream);
+        g_last_blocks = blocks;
+        g_last_lds = lds;
+        snprintf(g_last_buf, sizeof g_last_buf, "%s_k%d_nt", ks->name, P.k);
+        g_last = g_last_buf;
+        g_last_sym = F.body_sym();
+        return e == hipSuccess ? MPI_SUCCESS : MPI_ERR_OTHER;
+    }
     long work = P.vec_ok ? (P.nvec + unroll * 256 - 1) / (unroll * 256)
                          : (P.n + 255) / 256;
     if (work < 1) work = 1;
     const unsigned blocks = (unsigned)(work < g_block_cap ? work : g_block_cap);
     void *args[] = {&P};
-    hipError_t e = hipLaunchKernel(fn, dim3(blocks), dim3(256), args, 0, stream);
+    hipError_t e = hipLaunchKernel(fn, dim3(blocks), dim3(256), args, lds, stream);
+    g_last_blocks = blocks;
+    g_last_lds = lds;
     snprintf(g_last_buf, sizeof g_last_buf, "%s_k%d%s", ks->name, P.k, nt ? "_nt" : "");
     g_last = g_last_buf;
-    g_last_sym = syms[nt]();
+    g_last_sym = F.sym[nt]();
     return e == hipSuccess ? MPI_SUCCESS : MPI_ERR_OTHER;
 }
 
@@ -750,7 +881,7 @@ extern "C" int mvx_op_apply(int op, int dtype, const void *in, void *inout,
     P.dst = (char *)inout;
     P.n = (long)n;
     P.k = 2;
-    return launch(ks, ks->apply, ks->apply_sym, 4, P, (hipStream_t)stream);
+    return launch(ks, ks->apply, P, (hipStream_t)stream);
 }
 
 extern "C" int mvx_op_program(int op, int dtype, const void *const *srcs,
@@ -781,15 +912,16 @@ extern "C" int mvx_op_program(int op, int dtype, const void *const *srcs,
     if (k <= 2) {
         /* the only programs over <= 2 leaves: nothing, or y0 op y1 */
         if (k == 2 && !(tree_mask & 1u) && !(chain_mask & 2u)) return MPI_ERR_ARG;
-        return launch(ks, ks->apply, ks->apply_sym, 4, P, (hipStream_t)stream);
+        return launch(ks, ks->apply, P, (hipStream_t)stream);
     }
     init_env();
-    if (!g_generic_only && chain_mask == 0 && (k == 8 || k == 4) && tree_mask == mvx_tree_mask(k))
-        return k == 8 ? launch(ks, ks->tree8, ks->tree8_sym, 1, P, (hipStream_t)stream)
-                      : launch(ks, ks->tree4, ks->tree4_sym, 1, P, (hipStream_t)stream);
-    if (g_prog_u == 2 && ks->prog2[0])
-        return launch(ks, ks->prog2, ks->prog2_sym, 2, P, (hipStream_t)stream);
-    return launch(ks, ks->prog, ks->prog_sym, ks->prog_unroll, P, (hipStream_t)stream);
+    bool folded = false;
+    for (int q = 0; q < k; ++q) folded |= P.fold[q] != nullptr;
+    if (!g_generic_only && !folded && chain_mask == 0 && (k == 8 || k == 4) && tree_mask == mvx_tree_mask(k))
+        return launch(ks, k == 8 ? ks->tree8 : ks->tree4, P, (hipStream_t)stream);
+    if (g_prog_u == 2 && ks->prog2.fn[0])
+        return launch(ks, ks->prog2, P, (hipStream_t)stream);
+    return launch(ks, ks->prog, P, (hipStream_t)stream);
 }
 
 extern "C" unsigned mvx_tree_mask(int k)
@@ -829,3 +961,9 @@ extern "C" void mvx_hip_set_launch(int block_cap, int nt_min_bytes_log2)
 extern "C" const char *mvx_hip_last_kernel(void) { return g_last; }
 
 extern "C" const char *mvx_hip_last_kernel_symbol(void) { return g_last_sym; }
+
+extern "C" void mvx_hip_last_launch(unsigned *blocks, size_t *dynamic_lds)
+{
+    if (blocks) *blocks = g_last_blocks;
+    if (dynamic_lds) *dynamic_lds = g_last_lds;
+}
