@@ -158,8 +158,9 @@ void mvx_hip_set_launch(int block_cap, int nt_min_bytes_log2);
  * ("k_combine<2, float, 2, 4, 1>"). */
 const char *mvx_hip_last_kernel(void);
 const char *mvx_hip_last_kernel_symbol(void);
-/* grid blocks and dynamic LDS bytes (the residency cap) of the last launch */
-void mvx_hip_last_launch(unsigned *blocks, size_t *dynamic_lds);
+/* grid blocks, dynamic LDS bytes (the residency cap) and resident blocks per
+ * CU (the runtime's occupancy answer) of the last launch */
+void mvx_hip_last_launch(unsigned *blocks, size_t *dynamic_lds, int *blocks_per_cu);
 
 #ifdef __cplusplus
 }

@@ -428,11 +428,20 @@ struct BodyParams {
     long nvec;   // chunks
 };
 
+// 56 KiB of static LDS per block: 2 resident blocks (8 waves) per CU.
+// tools/tune_occ.hip, profiles/r02/tune_occ_lds.jsonl: the 8-leaf f32 tree
+// at U = 2 runs 47.8 / 94.5 us (8 x 32 / 64 MiB leaves, 79 / 80 % of HBM
+// peak) at 2 blocks per CU against 50.0 / 100.3 us at 3, 4 or 5 -- fewer,
+// fuller waves keep each HBM channel on fewer rows.  (LDS reservations of
+// 41-52 KiB, which the runtime's occupancy query calls 3 blocks per CU, run
+// like 3; 53 KiB and up like 2.)
+#define BODY_LDS_CAP (56 * 1024)
+
 template <int O, typename T, int KMAX, int U>
 __global__ void __launch_bounds__(256)
 k_tree_body(const BodyParams P)
 {
-    extern __shared__ char lds_cap[];
+    __shared__ char lds_cap[BODY_LDS_CAP];
     if (P.nvec < 0) lds_cap[threadIdx.x] = 0;
     constexpr int V = CG<T>::v;
     const long nthr = (long)gridDim.x * 256;
@@ -749,7 +758,7 @@ static int g_prog_u = 1;
 static int g_generic_only = 0;   // MVX_PROG_GENERIC=1: no fixed-tree kernels (A/B runs)
 // resident blocks per CU for the non-temporal launches of each family (0 =
 // as many as registers allow); MVX_CAP_{APPLY,PROG,TREE} override for A/B runs
-static int g_cap[FAM_N] = {0, 0, 3};
+static int g_cap[FAM_N] = {0, 0, 2};
 static int g_no_body = 0;        // MVX_NO_BODY=1: fixed trees through k_combine (A/B runs)
 static size_t g_cap_lds[FAM_N];
 static const char *g_last = "";
@@ -757,6 +766,7 @@ static char g_last_buf[96];
 static const char *g_last_sym = "";
 static unsigned g_last_blocks;
 static size_t g_last_lds;
+static const void *g_last_fn;
 
 static void init_env()
 {
@@ -781,10 +791,11 @@ static void init_env()
         e = getenv(caps[f]);
         if (e) g_cap[f] = atoi(e);
         // dynamic LDS per block that leaves room for g_cap blocks per CU and
-        // not one more (the kernels do not touch it); under 64 KiB needs no
-        // function attribute
-        g_cap_lds[f] = g_cap[f] >= 2 ? ((size_t)lds_per_cu / (size_t)g_cap[f] - 1024) & ~(size_t)1023 : 0;
-        if (g_cap_lds[f] > 64 * 1024) g_cap_lds[f] = 0;
+        // not one more (the kernels do not touch it): the middle of the
+        // range, 2 * LDS / (2 * cap + 1), clear of the allocator's rounding
+        // at the edges; at most 64 KiB (no function attribute needed)
+        g_cap_lds[f] = g_cap[f] >= 2 ? ((size_t)lds_per_cu * 2 / (size_t)(2 * g_cap[f] + 1)) & ~(size_t)1023 : 0;
+        if (g_cap_lds[f] > 64 * 1024) g_cap_lds[f] = 64 * 1024;
     }
 }
 
@@ -828,9 +839,10 @@ static int launch(const KSet *ks, const KFam &F, Params &P, hipStream_t stream)
         long work = (P.nvec + F.body_unroll * 256 - 1) / (F.body_unroll * 256);
         const unsigned blocks = (unsigned)(work < g_block_cap ? work : g_block_cap);
         void *bargs[] = {&B};
-        hipError_t e = hipLaunchKernel(F.body, dim3(blocks), dim3(256), bargs, lds, stream);
+        hipError_t e = hipLaunchKernel(F.body, dim3(blocks), dim3(256), bargs, 0, stream);
         g_last_blocks = blocks;
-        g_last_lds = lds;
+        g_last_lds = 0;
+        g_last_fn = F.body;
         snprintf(g_last_buf, sizeof g_last_buf, "%s_k%d_nt", ks->name, P.k);
         g_last = g_last_buf;
         g_last_sym = F.body_sym();
@@ -844,6 +856,7 @@ static int launch(const KSet *ks, const KFam &F, Params &P, hipStream_t stream)
     hipError_t e = hipLaunchKernel(fn, dim3(blocks), dim3(256), args, lds, stream);
     g_last_blocks = blocks;
     g_last_lds = lds;
+    g_last_fn = fn;
     snprintf(g_last_buf, sizeof g_last_buf, "%s_k%d%s", ks->name, P.k, nt ? "_nt" : "");
     g_last = g_last_buf;
     g_last_sym = F.sym[nt]();
@@ -962,8 +975,17 @@ extern "C" const char *mvx_hip_last_kernel(void) { return g_last; }
 
 extern "C" const char *mvx_hip_last_kernel_symbol(void) { return g_last_sym; }
 
-extern "C" void mvx_hip_last_launch(unsigned *blocks, size_t *dynamic_lds)
+extern "C" void mvx_hip_last_launch(unsigned *blocks, size_t *dynamic_lds, int *blocks_per_cu)
 {
     if (blocks) *blocks = g_last_blocks;
     if (dynamic_lds) *dynamic_lds = g_last_lds;
+    if (blocks_per_cu) {
+        int occ = 0;
+        if (!g_last_fn ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, g_last_fn, 256, g_last_lds) != hipSuccess) {
+            (void)hipGetLastError();
+            occ = 0;
+        }
+        *blocks_per_cu = occ;
+    }
 }

@@ -53,6 +53,37 @@ __global__ void __launch_bounds__(256) k_tree(P8 p)
     }
 }
 
+// the same loop with the residency cap as 52 KiB of static LDS (what the
+// product's k_tree_body does) instead of a dynamic reservation at launch
+template <int K, int U>
+__global__ void __launch_bounds__(256) k_tree_static(P8 p)
+{
+    __shared__ char lds_cap[52 * 1024];
+    if (p.nvec < 0) lds_cap[threadIdx.x] = 0;
+    const long nthr = (long)gridDim.x * 256;
+    for (long c0 = (long)blockIdx.x * 256 * U + threadIdx.x; c0 < p.nvec; c0 += nthr * U) {
+        f32x4 x[U][K];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const long c = c0 + (long)u * 256;
+            if (c < p.nvec)
+#pragma unroll
+                for (int q = 0; q < K; ++q) x[u][q] = __builtin_nontemporal_load(p.s[q] + c);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const long c = c0 + (long)u * 256;
+            if (c < p.nvec) {
+#pragma unroll
+                for (int h = 1; h < K; h <<= 1)
+#pragma unroll
+                    for (int q = 0; q + h < K; q += 2 * h) x[u][q] = x[u][q] + x[u][q + h];
+                __builtin_nontemporal_store(x[u][0], p.d + c);
+            }
+        }
+    }
+}
+
 typedef void (*KF)(P8);
 
 int main(int argc, char **argv)
@@ -93,6 +124,7 @@ int main(int argc, char **argv)
             for (int grid = 0; grid < 1; ++grid)   // persistent grids lost everywhere (first sweep)
                 for (int occ : occs) {
                     if (grid && !occ) continue;
+                    if (getenv("ONLY_U2CAP3") && (U != 2 || occ != 3)) continue;
                     const size_t lds = occ ? (size_t)(160 * 1024 / occ) & ~(size_t)1023 : 0;
                     if (lds > 64 * 1024 && hipFuncSetAttribute((const void *)f, hipFuncAttributeMaxDynamicSharedMemorySize,
                                                                (int)lds) != hipSuccess) {
@@ -131,6 +163,55 @@ int main(int argc, char **argv)
                     fflush(stdout);
                 }
         }
+        if (sh.k == 8 && getenv("LDS_SWEEP")) {   // U = 2, dynamic LDS from 24 to 80 KiB
+            const int kib[] = {24, 32, 40, 41, 44, 48, 50, 52, 53, 54, 56, 60, 64, 72, 80};
+            for (int kb : kib) {
+                const size_t lds = (size_t)kb * 1024;
+                if (lds > 64 * 1024 && hipFuncSetAttribute((const void *)k_tree<8, 2>,
+                                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {
+                    (void)hipGetLastError();
+                    continue;
+                }
+                int real = 0;
+                CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&real, (const void *)k_tree<8, 2>, 256, lds));
+                std::vector<float> t;
+                const long blocks = ps[0].nvec / 512;
+                for (int r = 0; r < 5; ++r) {
+                    for (int w = 0; w < 3; ++w) hipLaunchKernelGGL((k_tree<8, 2>), dim3(blocks), dim3(256), lds, 0, ps[w % sh.sets]);
+                    CHECK(hipEventRecord(e0, 0));
+                    for (int i = 0; i < 20; ++i) hipLaunchKernelGGL((k_tree<8, 2>), dim3(blocks), dim3(256), lds, 0, ps[i % sh.sets]);
+                    CHECK(hipEventRecord(e1, 0));
+                    CHECK(hipEventSynchronize(e1));
+                    float ms;
+                    CHECK(hipEventElapsedTime(&ms, e0, e1));
+                    t.push_back(ms / 20);
+                }
+                std::sort(t.begin(), t.end());
+                const double med = t[t.size() / 2], bytes = (double)(sh.k + 1) * sh.leaf;
+                printf("{\"k\": %d, \"leaf_mib\": %ld, \"variant\": \"U2 dynamic lds %d KiB\", \"blocks_per_cu\": %d, "
+                       "\"us\": %.2f, \"frac\": %.4f}\n", sh.k, sh.leaf >> 20, kb, real, med * 1e3,
+                       bytes / (med * 1e-3) / 8e12);
+                fflush(stdout);
+            }
+        }
+        if (sh.k == 8) {   // static-LDS variant of U = 2
+            std::vector<float> t;
+            const long blocks = ps[0].nvec / 512;
+            for (int r = 0; r < 5; ++r) {
+                for (int w = 0; w < 3; ++w) hipLaunchKernelGGL((k_tree_static<8, 2>), dim3(blocks), dim3(256), 0, 0, ps[w % sh.sets]);
+                CHECK(hipEventRecord(e0, 0));
+                for (int i = 0; i < 20; ++i) hipLaunchKernelGGL((k_tree_static<8, 2>), dim3(blocks), dim3(256), 0, 0, ps[i % sh.sets]);
+                CHECK(hipEventRecord(e1, 0));
+                CHECK(hipEventSynchronize(e1));
+                float ms;
+                CHECK(hipEventElapsedTime(&ms, e0, e1));
+                t.push_back(ms / 20);
+            }
+            std::sort(t.begin(), t.end());
+            const double med = t[t.size() / 2], bytes = (double)(sh.k + 1) * sh.leaf;
+            printf("{\"k\": %d, \"leaf_mib\": %ld, \"variant\": \"static-lds U2\", \"us\": %.2f, \"frac\": %.4f}\n",
+                   sh.k, sh.leaf >> 20, med * 1e3, bytes / (med * 1e-3) / 8e12);
+        }
         {   // the product kernel (mvx_op_combine: the launched template and
             // residency of libmvx_hip.so) on exactly these buffers
             std::vector<float> t;
@@ -156,10 +237,11 @@ int main(int argc, char **argv)
             const double med = t[t.size() / 2], bytes = (double)(sh.k + 1) * sh.leaf;
             unsigned lb = 0;
             size_t ll = 0;
-            mvx_hip_last_launch(&lb, &ll);
+            int locc = 0;
+            mvx_hip_last_launch(&lb, &ll, &locc);
             printf("{\"k\": %d, \"leaf_mib\": %ld, \"variant\": \"product %s\", \"blocks\": %u, \"lds\": %zu, "
-                   "\"us\": %.2f, \"frac\": %.4f}\n",
-                   sh.k, sh.leaf >> 20, mvx_hip_last_kernel_symbol(), lb, ll, med * 1e3, bytes / (med * 1e-3) / 8e12);
+                   "\"blocks_per_cu\": %d, \"us\": %.2f, \"frac\": %.4f}\n",
+                   sh.k, sh.leaf >> 20, mvx_hip_last_kernel_symbol(), lb, ll, locc, med * 1e3, bytes / (med * 1e-3) / 8e12);
             fflush(stdout);
         }
         for (char *b : bigs) CHECK(hipFree(b));
