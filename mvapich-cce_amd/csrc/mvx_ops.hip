@@ -470,6 +470,39 @@ k_tree_body(const BodyParams P)
     }
 }
 
+// The same over a full CHAIN ((y0 op y1) op y2) ..., the pairwise
+// Reduce_scatter's order (C4: k = 4, p = 4)
+template <int O, typename T, int KMAX, int U>
+__global__ void __launch_bounds__(256)
+k_chain_body(const BodyParams P)
+{
+    __shared__ char lds_cap[BODY_LDS_CAP];
+    if (P.nvec < 0) lds_cap[threadIdx.x] = 0;
+    constexpr int V = CG<T>::v;
+    const long nthr = (long)gridDim.x * 256;
+    for (long c0 = (long)blockIdx.x * (256 * U) + threadIdx.x; c0 < P.nvec; c0 += nthr * U) {
+        Chunk<T> x[U][KMAX];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const long c = c0 + (long)u * 256;
+            if (c < P.nvec)
+#pragma unroll
+                for (int q = 0; q < KMAX; ++q) x[u][q] = ld_chunk<T, 1>(P.src[q], c);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const long c = c0 + (long)u * 256;
+            if (c < P.nvec) {
+#pragma unroll
+                for (int q = 1; q < KMAX; ++q)
+#pragma unroll
+                    for (int j = 0; j < V; ++j) x[u][0].e[j] = F<O, T>::f(x[u][0].e[j], x[u][q].e[j]);
+                st_chunk<T, 1>(P.dst, c, x[u][0]);
+            }
+        }
+    }
+}
+
 }  // namespace mvx
 
 // ---------------------------------------------------------------------------
@@ -499,6 +532,21 @@ static const char *ksym()
 }
 
 typedef const char *(*SymFn)();
+
+template <int O, typename T, int KMAX, int U>
+static const char *ksym_chain_body()
+{
+    static char buf[160];
+    if (!buf[0]) {
+        const char *pf = __PRETTY_FUNCTION__;
+        const char *t = strstr(pf, "T = ");
+        const char *e = t ? strstr(t, ", KMAX") : nullptr;
+        const int tl = (t && e) ? (int)(e - t - 4) : 1;
+        const char *tn = (t && e) ? t + 4 : "?";
+        snprintf(buf, sizeof buf, "k_chain_body<%d, %.*s, %d, %d>", O, tl, tn, KMAX, U);
+    }
+    return buf;
+}
 
 template <int O, typename T, int KMAX, int U>
 static const char *ksym_body()
@@ -533,6 +581,7 @@ struct KSet {
     KFam prog;             // KMAX 8 combine program (masks)
     KFam prog2;            // 4-byte types: the U = 2 program (MVX_PROG_U=2); fn[0] null otherwise
     KFam tree8, tree4;     // PROG = 1: full trees over 8 / 4 leaves
+    KFam chain8, chain4;   // full chains over 8 / 4 leaves: k_chain_body, else the masked program
     int esize;
     int chunk;             // bytes per chunk (16, or the element if wider)
     const char *name;
@@ -561,15 +610,26 @@ static KFam kfam(int fam)
     return f;
 }
 
+// a full chain: the masked program, with k_chain_body for large aligned launches
+template <int O, typename T, int KMAX>
+static KFam kchain()
+{
+    KFam f = kfam<O, T, MVX_COMBINE_KMAX, 1, 1, 0>(FAM_PROG);
+    f.body = (const void *)&k_chain_body<O, T, KMAX, 2>;
+    f.body_sym = &ksym_chain_body<O, T, KMAX, 2>;
+    f.body_unroll = 2;
+    return f;
+}
+
 // Chunks in flight per lane, and (launch()) resident blocks per CU, for the
 // non-temporal (large) launches -- round 2, tools/tune_occ.hip,
 // profiles/r02/tune_occ.jsonl: at full occupancy a streaming launch keeps ~10x
 // the bytes in flight Little's law needs and every HBM channel juggles rows
 // from all the streams; fewer resident blocks with more loads each measured
-// k = 8, 8 x 32 MiB: U1 uncapped 76.5 %, U2 at 3 blocks / CU 79.0 %;
-// k = 8, 8 x 64 MiB: 77.0 % -> 79.6 %.  The plain op (k = 2) gains nothing
-// reproducible from a cap and keeps U = 4 at full occupancy, as do the
-// cached (small-launch) builds.
+// k = 8, 8 x 32 MiB: U1 uncapped 76.5 %, U2 at 2 blocks / CU 79.0 %;
+// k = 8, 8 x 64 MiB: 77.0 % -> 79.9 % (BODY_LDS_CAP).  The plain op (k = 2)
+// and the masked program gain nothing from a cap and keep U = 4 / 1 at full
+// occupancy, as do the cached (small-launch) builds.
 template <int O, typename T>
 static KSet kset(const char *name)
 {
@@ -578,6 +638,8 @@ static KSet kset(const char *name)
     s.prog = kfam<O, T, MVX_COMBINE_KMAX, 1, 1, 0>(FAM_PROG);
     s.tree8 = kfam<O, T, 8, 1, 2, 1>(FAM_TREE);
     s.tree4 = kfam<O, T, 4, 1, 2, 1>(FAM_TREE);
+    s.chain8 = kchain<O, T, 8>();
+    s.chain4 = kchain<O, T, 4>();
     if constexpr (sizeof(T) == 4) {
         s.prog2 = kfam<O, T, MVX_COMBINE_KMAX, 2, 2, 0>(FAM_PROG);
     } else {
@@ -932,6 +994,8 @@ extern "C" int mvx_op_program(int op, int dtype, const void *const *srcs,
     for (int q = 0; q < k; ++q) folded |= P.fold[q] != nullptr;
     if (!g_generic_only && !folded && chain_mask == 0 && (k == 8 || k == 4) && tree_mask == mvx_tree_mask(k))
         return launch(ks, k == 8 ? ks->tree8 : ks->tree4, P, (hipStream_t)stream);
+    if (!g_generic_only && !folded && tree_mask == 0 && (k == 8 || k == 4) && chain_mask == mvx_chain_mask(k))
+        return launch(ks, k == 8 ? ks->chain8 : ks->chain4, P, (hipStream_t)stream);
     if (g_prog_u == 2 && ks->prog2.fn[0])
         return launch(ks, ks->prog2, P, (hipStream_t)stream);
     return launch(ks, ks->prog, P, (hipStream_t)stream);

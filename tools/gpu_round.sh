@@ -58,6 +58,6 @@ if [[ $STAGE == pmc_kernels ]]; then
   run timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmck_f -o f -- python3 tools/bench_kernels.py > gpurun_out/pmck_f.log 2>&1 || exit 1
   run timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmck_w -o w -- python3 tools/bench_kernels.py > gpurun_out/pmck_w.log 2>&1 || exit 1
   python3 tools/pmc_summary.py gpurun_out/pmck_f gpurun_out/pmck_w "k_tree_body<2, float, 8, 2>" sum_f32_k8_nt 33554432 301989888 gpurun_out/pmc_c3.json && \
-  python3 tools/pmc_summary.py gpurun_out/pmck_f gpurun_out/pmck_w "k_combine<5, unsigned long, 8, 1, 1, 0>" band_u64_k4_nt 268435456 1342177280 gpurun_out/pmc_c4.json && \
+  python3 tools/pmc_summary.py gpurun_out/pmck_f gpurun_out/pmck_w "k_chain_body<5, unsigned long, 4, 2>" band_u64_k4_nt 268435456 1342177280 gpurun_out/pmc_c4.json && \
   python3 tools/pmc_summary.py gpurun_out/pmck_f gpurun_out/pmck_w "k_tree_body<11, mvx::pfi, 8, 2>" maxloc_float_int_k8_nt 67108864 603979776 gpurun_out/pmc_c5.json || exit 1
 fi
