@@ -571,9 +571,10 @@ struct KFam {
     SymFn sym[2];
     int unroll[2];
     int fam;
-    const void *body;      // FAM_TREE: k_tree_body for large aligned launches, or null
+    const void *body;      // k_tree_body / k_chain_body for large aligned launches, or null
     SymFn body_sym;
     int body_unroll;
+    int body_k;            // the body kernel's leaf count (launches with other k never use it)
 };
 
 struct KSet {
@@ -602,10 +603,12 @@ static KFam kfam(int fam)
         f.body = (const void *)&k_tree_body<O, T, KMAX, U1>;
         f.body_sym = &ksym_body<O, T, KMAX, U1>;
         f.body_unroll = U1;
+        f.body_k = KMAX;
     } else {
         f.body = nullptr;
         f.body_sym = nullptr;
         f.body_unroll = 0;
+        f.body_k = 0;
     }
     return f;
 }
@@ -618,6 +621,7 @@ static KFam kchain()
     f.body = (const void *)&k_chain_body<O, T, KMAX, 2>;
     f.body_sym = &ksym_chain_body<O, T, KMAX, 2>;
     f.body_unroll = 2;
+    f.body_k = KMAX;
     return f;
 }
 
@@ -635,6 +639,9 @@ static KSet kset(const char *name)
 {
     KSet s;
     s.apply = kfam<O, T, 2, 4, 4, 0>(FAM_APPLY);
+    // (a 2-leaf body at U = 3 and 2 blocks per CU ran 123.8 vs 126.4 us in
+    // the standalone sweep, profiles/r02/tune_occ_k2.jsonl, but 124.8 vs
+    // 123.5-124.8 us in the product: not adopted)
     s.prog = kfam<O, T, MVX_COMBINE_KMAX, 1, 1, 0>(FAM_PROG);
     s.tree8 = kfam<O, T, 8, 1, 2, 1>(FAM_TREE);
     s.tree4 = kfam<O, T, 4, 1, 2, 1>(FAM_TREE);
@@ -891,8 +898,8 @@ static int launch(const KSet *ks, const KFam &F, Params &P, hipStream_t stream)
     }
     bool folded = false;
     for (int q = 0; q < P.k; ++q) folded |= P.fold[q] != nullptr;
-    if (nt && F.body && !g_no_body && P.vec_ok && P.head == 0 && P.nvec > 0 && P.nvec * ks->chunk == P.n * es &&
-        !folded) {
+    if (nt && F.body && !g_no_body && P.k == F.body_k && P.vec_ok && P.head == 0 && P.nvec > 0 &&
+        P.nvec * ks->chunk == P.n * es && !folded) {
         BodyParams B;
         memset(&B, 0, sizeof B);
         for (int q = 0; q < P.k; ++q) B.src[q] = reinterpret_cast<const u32x4 *>(P.src[q]);

@@ -163,6 +163,41 @@ int main(int argc, char **argv)
                     fflush(stdout);
                 }
         }
+        if (sh.k == 2 && getenv("K2_SWEEP")) {   // the plain op: U x resident blocks (by LDS reservation)
+            const int kib[] = {0, 36, 44, 56, 88};   // ~ 8 (regs), 4, 3, 2, 1 blocks per CU
+            KF fs[] = {k_tree<2, 1>, k_tree<2, 2>, k_tree<2, 3>, k_tree<2, 4>, k_tree<2, 6>};
+            const int us[] = {1, 2, 3, 4, 6};
+            for (int ui = 0; ui < 5; ++ui)
+                for (int kb : kib) {
+                    KF f = fs[ui];
+                    const size_t lds = (size_t)kb * 1024;
+                    if (lds > 64 * 1024 && hipFuncSetAttribute((const void *)f, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                               (int)lds) != hipSuccess) {
+                        (void)hipGetLastError();
+                        continue;
+                    }
+                    int real = 0;
+                    CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&real, (const void *)f, 256, lds));
+                    std::vector<float> t;
+                    const long blocks = (ps[0].nvec + 256L * us[ui] - 1) / (256L * us[ui]);
+                    for (int r = 0; r < 5; ++r) {
+                        for (int w = 0; w < 3; ++w) hipLaunchKernelGGL(f, dim3(blocks), dim3(256), lds, 0, ps[w % sh.sets]);
+                        CHECK(hipEventRecord(e0, 0));
+                        for (int i = 0; i < 20; ++i) hipLaunchKernelGGL(f, dim3(blocks), dim3(256), lds, 0, ps[i % sh.sets]);
+                        CHECK(hipEventRecord(e1, 0));
+                        CHECK(hipEventSynchronize(e1));
+                        float ms;
+                        CHECK(hipEventElapsedTime(&ms, e0, e1));
+                        t.push_back(ms / 20);
+                    }
+                    std::sort(t.begin(), t.end());
+                    const double med = t[t.size() / 2], bytes = (double)(sh.k + 1) * sh.leaf;
+                    printf("{\"k\": 2, \"leaf_mib\": %ld, \"variant\": \"U%d lds %d KiB\", \"blocks_per_cu\": %d, "
+                           "\"us\": %.2f, \"frac\": %.4f}\n", sh.leaf >> 20, us[ui], kb, real, med * 1e3,
+                           bytes / (med * 1e-3) / 8e12);
+                    fflush(stdout);
+                }
+        }
         if (sh.k == 8 && getenv("LDS_SWEEP")) {   // U = 2, dynamic LDS from 24 to 80 KiB
             const int kib[] = {24, 32, 40, 41, 44, 48, 50, 52, 53, 54, 56, 60, 64, 72, 80};
             for (int kb : kib) {
