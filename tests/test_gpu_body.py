@@ -1,0 +1,84 @@
+"""The body kernels (k_tree_body / k_chain_body, mvx_ops.hip): large aligned
+full trees and chains over 4 or 8 unfolded leaves run a lean loop at 2
+resident blocks per CU; everything else (a head or tail outside the 16-byte
+body, misaligned leaves, folded leaves, small launches, MVX_NO_BODY) runs
+k_combine.  Both must give the oracle's bits, and the dispatch must pick the
+kernel it claims to (mvx_hip_last_kernel_symbol)."""
+import ctypes
+
+import numpy as np
+import pytest
+
+import mvxtest as T
+from plan_exec import SHAPE_CHAIN, SHAPE_TREE, combine_cpu
+
+pytestmark = pytest.mark.gpu
+
+NT_ELEMS = 4 << 20          # 16 MiB of f32 per leaf: a non-temporal launch at k >= 4
+
+
+def _run(mvx, op, dtype, k, shape, n, offset=0, folded=False, seed=0):
+    import torch
+    E = mvx.dtype_info(dtype)[0]
+    S = [T.rand_vec(dtype, n, 100 * seed + q) for q in range(k)]
+    F = [T.rand_vec(dtype, n, 100 * seed + 50 + q) if folded and q % 2 else None for q in range(k)]
+    # device leaves at byte `offset` into their allocation (offset 4 breaks the
+    # 16-byte body for 4-byte types: head elements, k_combine)
+    def dev(x):
+        b = torch.zeros(x.nbytes + 64, dtype=torch.uint8, device="cuda")
+        b[offset:offset + x.nbytes] = torch.from_numpy(x.view(np.uint8).copy()).cuda()
+        return b[offset:offset + x.nbytes]
+    dS = [dev(x) for x in S]
+    dF = [dev(x) if x is not None else None for x in F]
+    dst = dev(np.zeros(n, S[0].dtype))
+    folds = dF if folded else None
+    rc = mvx.op_combine(op, dtype, dS, dst, n, shape=shape, folds=folds)
+    torch.cuda.synchronize()
+    assert rc == 0
+    sym = mvx.last_kernel_symbol()
+    ref = combine_cpu(op, dtype, E, [x.view(np.uint8) for x in S],
+                      [x.view(np.uint8) if x is not None else None for x in F], shape, n)
+    return sym, T.from_dev(dst).view(np.uint8), ref
+
+
+@pytest.mark.parametrize("k", [4, 8])
+@pytest.mark.parametrize("shape", [SHAPE_TREE, SHAPE_CHAIN])
+@pytest.mark.parametrize("op,dtype", [(102, 10), (111, 17), (105, 8), (100, 11)])
+def test_body_dispatch_and_bits(mvx, op, dtype, k, shape):
+    E = mvx.dtype_info(dtype)[0]
+    n = NT_ELEMS * 4 // E
+    want = "k_tree_body<" if shape == SHAPE_TREE else "k_chain_body<"
+    sym, got, ref = _run(mvx, op, dtype, k, shape, n)
+    assert sym.startswith(want), sym
+    assert np.array_equal(got, ref)
+    # a ragged tail (not a whole number of 16-byte chunks) or a shifted
+    # start: the general kernel
+    for n2, off in ((n + 1 if E < 16 else n, 0), (n, 4 if E == 4 else 8)):
+        if (n2, off) == (n, 0):
+            continue
+        sym, got, ref = _run(mvx, op, dtype, k, shape, n2, offset=off, seed=1)
+        assert sym.startswith("k_combine<"), sym
+        assert np.array_equal(got, ref)
+
+
+def test_body_not_used_for_folds_small_or_disabled(mvx, monkeypatch):
+    n = NT_ELEMS
+    sym, got, ref = _run(mvx, 102, 10, 8, SHAPE_TREE, n, folded=True)
+    assert sym.startswith("k_combine<") and np.array_equal(got, ref)
+    sym, got, ref = _run(mvx, 102, 10, 8, SHAPE_TREE, 4096)      # cached launch
+    assert sym.startswith("k_combine<") and np.array_equal(got, ref)
+
+
+def test_launch_residency_reported(mvx):
+    """mvx_hip_last_launch: the body kernels hold 2 blocks per CU; the plain
+    op is uncapped (8)."""
+    lib = mvx.hip()
+    lib.mvx_hip_last_launch.argtypes = [ctypes.POINTER(ctypes.c_uint), ctypes.POINTER(ctypes.c_size_t),
+                                        ctypes.POINTER(ctypes.c_int)]
+    b, lds, occ = ctypes.c_uint(), ctypes.c_size_t(), ctypes.c_int()
+    _run(mvx, 102, 10, 8, SHAPE_TREE, NT_ELEMS)
+    lib.mvx_hip_last_launch(ctypes.byref(b), ctypes.byref(lds), ctypes.byref(occ))
+    assert occ.value == 2 and b.value == NT_ELEMS // 4 // 512
+    _run(mvx, 102, 10, 2, SHAPE_TREE, NT_ELEMS * 8)
+    lib.mvx_hip_last_launch(ctypes.byref(b), ctypes.byref(lds), ctypes.byref(occ))
+    assert occ.value == 8 and lds.value == 0
