@@ -185,3 +185,52 @@ def test_undefined_ops_and_refused_layouts(mvx, oracle, types):
     assert r == mvx.MPI_ERR_TYPE
     mvx.MPI_Type_free(odd)
     comm.free()
+
+
+@pytest.mark.parametrize("where", ["device", "host"])
+@pytest.mark.parametrize("p", [2, 3, 5, 8])
+@pytest.mark.parametrize("tname,op,kind", CASES)
+def test_struct_collectives_smp_flavour(mvx, oracle, types, where, p, tname, op, kind):
+    """The _SMP_ collops on derived types: below the shmem thresholds (int
+    count * extent < 32 KiB Allreduce, 1 KiB Reduce) the node leader's
+    rank-order fold, above them the intra_* algorithms -- against the
+    oracle's replay of intra_shmem_* (smp = 1)."""
+    import torch
+    h = types[tname]
+    ext = mvx.MPI_Type_extent(h)[1]
+    comm = mvx.Comm.local_ranks(p, 0)
+    assert comm.set_tuning(mvx.smp_tuning()) == 0
+    oracle.smp_set(1)
+    uop = None
+    if op == "idsum":
+        rc, uop = (mvx.op_create_device(uops.dev_fn("idsum"), 1) if where == "device"
+                   else mvx.MPI_Op_create(uops.host_fn("idsum"), 1))
+        assert rc == 0
+        assert oracle.user_op_set(250, uops.host_fn("idsum"), 1) == 0
+    try:
+        for coll in ("ar", "red"):
+            for n in (3, (1 << 10) // ext - 1, (1 << 10) // ext + 1, (1 << 15) // ext - 1, (1 << 15) // ext + 1):
+                S = [_pairs_bytes(h, n, ext, 29 * p + r + n, kind) for r in range(p)]
+                R0 = [np.full(n * ext, 0x5C, np.uint8) for _ in range(p)]
+                if where == "device":
+                    sends = [torch.from_numpy(s).cuda() for s in S]
+                    recvs = [torch.from_numpy(r.copy()).cuda() for r in R0]
+                else:
+                    sends = [s.copy() for s in S]
+                    recvs = [r.copy() for r in R0]
+                root = p - 1
+                r, rcs = _coll(comm, coll, sends, recvs, n, h, uop if uop else op, root)
+                assert r == 0, (coll, n, r)
+                ref = [x.copy() for x in R0]
+                rref = _oracle(oracle, coll, S, ref, n, h, 250 if uop else op, root)
+                assert rcs == rref, (coll, n, rcs, rref)
+                for q in range(p):
+                    if coll == "red" and q != root:
+                        continue
+                    got = recvs[q] if isinstance(recvs[q], np.ndarray) else T.from_dev(recvs[q])
+                    assert np.array_equal(got, ref[q]), (tname, op, coll, n, q)
+    finally:
+        oracle.smp_set(0)
+        comm.free()
+        if uop:
+            mvx.MPI_Op_free(uop)
