@@ -43,7 +43,7 @@ CONFIGS = {
     "c4": ("reduce_scatter", MPI_LONG, MPI_BAND, 8, 1024, "MPI_Reduce_scatter MPI_BAND MPI_LONG"),
     "c5": ("allreduce", MPI_FLOAT_INT, MPI_MAXLOC, 8, 512, "MPI_Allreduce MPI_MAXLOC MPI_FLOAT_INT"),
 }
-EXCH = {"p2p": (0, 0), "pipe": (1, 4), "coll": (2, 0)}
+EXCH = {"p2p": (0, 0), "pipe": (1, 4), "pipe2": (1, 2), "pipe8": (1, 8), "coll": (2, 0)}
 
 
 def parse():
@@ -64,7 +64,7 @@ def parse():
     ap.add_argument("--sets", type=int, default=4,
                     help="input sets used round-robin (4 x 512 MiB keeps every step out of the 256 MiB "
                          "Infinity Cache: the number is HBM-bound, not cache-bound)")
-    ap.add_argument("--exchange", default="auto", choices=["auto", "p2p", "pipe", "coll"])
+    ap.add_argument("--exchange", default="auto", choices=["auto", "p2p", "pipe", "pipe2", "pipe8", "coll"])
     ap.add_argument("--tune-steps", type=int, default=5)
     ap.add_argument("--transport", default="rccl", choices=["rccl", "host"],
                     help="host: ranks may share a GPU, bytes move through gloo (a test of the "
@@ -379,7 +379,7 @@ def run_multi(args, mvx, dev, world, rank, local):
 
     # exchange variants: timed, the fastest chosen on rank 0; each reports
     # its parity against the reference
-    names = ["p2p", "pipe", "coll"] if args.exchange == "auto" else [args.exchange]
+    names = list(EXCH) if args.exchange == "auto" else [args.exchange]
     tried = {}
     for name in names:
         mode, slices = EXCH[name]
