@@ -1,6 +1,6 @@
 """mvapich-cce_amd -- MI355X-native MPI reduction path (Python host mirror).
 
-The product is two in-tree shared libraries built from ``csrc/``:
+The product is in-tree shared libraries built from ``csrc/``:
 
 * ``libmvx_hip.so`` -- hand-written HIP kernels for gfx950 behind the C-ABI of
   ``include/mvx_hip.h`` (``mvx_op_apply``, ``mvx_op_combine``, ...);
@@ -8,7 +8,10 @@ The product is two in-tree shared libraries built from ``csrc/``:
   ``MPI_Reduce`` / ``MPI_Allreduce`` / ``MPI_Reduce_scatter`` /
   ``MPI_Op_create`` / ``MPI_Op_free`` / ``MPIR_SUM`` ... with the reference's
   handles and error codes, plans in the reference's combine order, RCCL for
-  the data movement.
+  the data movement;
+* ``libmvx_embed.so`` -- the same host library exporting only ``mvx_*``
+  names (``include/mvx_embed.h``), for linking into MVAPICH itself
+  (``integration/intra_mvx.c``).
 
 This module binds them with ctypes and mirrors the reference's C interface
 (same function names, argument meaning and return codes) so tests read like
@@ -121,6 +124,9 @@ def _load():
     _hip.mvx_hip_set_launch.restype = None
     _hip.mvx_hip_last_kernel.restype = ctypes.c_char_p
     _hip.mvx_hip_last_kernel_symbol.restype = ctypes.c_char_p
+    _hip.mvx_hip_last_launch.argtypes = [ctypes.POINTER(ctypes.c_uint), ctypes.POINTER(ctypes.c_size_t),
+                                         ctypes.POINTER(ctypes.c_int)]
+    _hip.mvx_hip_last_launch.restype = None
     c = _coll
     c.mvx_get_unique_id.argtypes = [vp]
     c.mvx_comm_init.argtypes = [pi, i, i, i, vp]

@@ -12,7 +12,7 @@ from .consts import COLL_ALLREDUCE, COLL_REDUCE, COLL_REDUCE_SCATTER  # noqa: F4
 __all__ = [
     "addr", "stream_handle", "op_apply", "op_combine", "op_program", "Comm",
     "MPI_Allreduce", "MPI_Reduce", "MPI_Reduce_scatter", "MPI_Scan", "MPI_Op_create", "MPI_Op_free", "op_create_device",
-    "MPIR_call", "op_errno", "last_kernel", "last_kernel_symbol", "set_launch",
+    "MPIR_call", "op_errno", "last_kernel", "last_kernel_symbol", "last_launch", "set_launch",
     "MPI_Type_contiguous", "MPI_Type_commit", "MPI_Type_free", "MPI_Type_extent", "MPI_Type_size",
     "MPI_Type_vector", "MPI_Type_hvector", "MPI_Type_indexed", "MPI_Type_hindexed", "MPI_Type_struct",
     "MPI_Type_lb", "MPI_Type_ub", "type_layout", "type_set_handle", "type_pack", "type_unpack",
@@ -79,6 +79,13 @@ def last_kernel():
 def last_kernel_symbol():
     """The last launched kernel template, as rocprofv3 names it."""
     return hip().mvx_hip_last_kernel_symbol().decode()
+
+
+def last_launch():
+    """(grid blocks, dynamic LDS bytes, resident blocks per CU) of the last launch."""
+    b, lds, occ = ctypes.c_uint(), ctypes.c_size_t(), ctypes.c_int()
+    hip().mvx_hip_last_launch(ctypes.byref(b), ctypes.byref(lds), ctypes.byref(occ))
+    return b.value, lds.value, occ.value
 
 
 # ------------------------------------------------------------- communicators

@@ -28,6 +28,22 @@ def test_every_declared_symbol_is_exported(mvx, header, lib):
     assert not missing, missing
 
 
+def test_embed_library_exports_only_mvx_names(mvx):
+    """libmvx_embed.so (csrc/embed.map): every function include/mvx_embed.h
+    declares, and no MPI_ / PMPI_ / MPIR_ symbol that could collide with the
+    host MPI's own when linked into MVAPICH (integration/intra_mvx.c)."""
+    import subprocess
+    so = os.path.join(ROOT, "mvapich-cce_amd", "libmvx_embed.so")
+    out = subprocess.check_output(["nm", "-D", "--defined-only", so], text=True)
+    syms = {line.split()[-1] for line in out.splitlines() if line.strip()}
+    names = declared("mvx_embed.h")
+    assert len(names) >= 15
+    assert set(names) <= syms, sorted(set(names) - syms)
+    bad = sorted(x for x in syms if re.match(r"(P?MPI_|MPIR_)", x))
+    assert not bad, bad
+    assert all(x.startswith(("mvx_", "MVX_")) for x in syms if not x.startswith("_")), sorted(syms)[:20]
+
+
 def test_collops_table_exported(mvx):
     assert ctypes.c_void_p.in_dll(mvx.coll(), "MVX_device_collops") is not None
 

@@ -4,8 +4,6 @@ resident blocks per CU; everything else (a head or tail outside the 16-byte
 body, misaligned leaves, folded leaves, small launches, MVX_NO_BODY) runs
 k_combine.  Both must give the oracle's bits, and the dispatch must pick the
 kernel it claims to (mvx_hip_last_kernel_symbol)."""
-import ctypes
-
 import numpy as np
 import pytest
 
@@ -72,13 +70,9 @@ def test_body_not_used_for_folds_small_or_disabled(mvx, monkeypatch):
 def test_launch_residency_reported(mvx):
     """mvx_hip_last_launch: the body kernels hold 2 blocks per CU; the plain
     op is uncapped (8)."""
-    lib = mvx.hip()
-    lib.mvx_hip_last_launch.argtypes = [ctypes.POINTER(ctypes.c_uint), ctypes.POINTER(ctypes.c_size_t),
-                                        ctypes.POINTER(ctypes.c_int)]
-    b, lds, occ = ctypes.c_uint(), ctypes.c_size_t(), ctypes.c_int()
     _run(mvx, 102, 10, 8, SHAPE_TREE, NT_ELEMS)
-    lib.mvx_hip_last_launch(ctypes.byref(b), ctypes.byref(lds), ctypes.byref(occ))
-    assert occ.value == 2 and b.value == NT_ELEMS // 4 // 512
+    blocks, lds, occ = mvx.last_launch()
+    assert occ == 2 and blocks == NT_ELEMS // 4 // 512
     _run(mvx, 102, 10, 2, SHAPE_TREE, NT_ELEMS * 8)
-    lib.mvx_hip_last_launch(ctypes.byref(b), ctypes.byref(lds), ctypes.byref(occ))
-    assert occ.value == 8 and lds.value == 0
+    blocks, lds, occ = mvx.last_launch()
+    assert occ == 8 and lds == 0
