@@ -65,6 +65,16 @@ static_assert(sizeof(pp<int8_t>) == 2 && sizeof(pp<double>) == 16, "");
 using xf::xf80;
 using xf::pxi;
 static_assert(sizeof(xf80) == 16 && sizeof(pxi) == 32, "");
+template <typename B> struct pp;
+
+// the x87 types: every op is dozens of integer instructions, so their
+// combines are ALU-bound and keep full occupancy (no body kernels, no
+// residency cap: the 8-leaf x87 SUM tree ran 109.7 us at 2 blocks per CU
+// against 74.4 us uncapped, profiles/r02/bench_kernels_x87.jsonl)
+template <typename T> struct alu_heavy { static constexpr bool v = false; };
+template <> struct alu_heavy<xf80> { static constexpr bool v = true; };
+template <> struct alu_heavy<pxi> { static constexpr bool v = true; };
+template <> struct alu_heavy<pp<xf80>> { static constexpr bool v = true; };
 
 // ---------------------------------------------------------------------------
 // the ops: F<op, T>::f(a, b) returns the new inout value (a = inout, b = in)
@@ -598,8 +608,8 @@ static KFam kfam(int fam)
     f.sym[1] = &ksym<O, T, KMAX, U1, 1, PROG>;
     f.unroll[0] = U0;
     f.unroll[1] = U1;
-    f.fam = fam;
-    if constexpr (PROG == 1) {
+    f.fam = (fam == FAM_TREE && alu_heavy<T>::v) ? FAM_PROG : fam;
+    if constexpr (PROG == 1 && !alu_heavy<T>::v) {
         f.body = (const void *)&k_tree_body<O, T, KMAX, U1>;
         f.body_sym = &ksym_body<O, T, KMAX, U1>;
         f.body_unroll = U1;
@@ -618,10 +628,12 @@ template <int O, typename T, int KMAX>
 static KFam kchain()
 {
     KFam f = kfam<O, T, MVX_COMBINE_KMAX, 1, 1, 0>(FAM_PROG);
-    f.body = (const void *)&k_chain_body<O, T, KMAX, 2>;
-    f.body_sym = &ksym_chain_body<O, T, KMAX, 2>;
-    f.body_unroll = 2;
-    f.body_k = KMAX;
+    if constexpr (!alu_heavy<T>::v) {
+        f.body = (const void *)&k_chain_body<O, T, KMAX, 2>;
+        f.body_sym = &ksym_chain_body<O, T, KMAX, 2>;
+        f.body_unroll = 2;
+        f.body_k = KMAX;
+    }
     return f;
 }
 
