@@ -191,3 +191,38 @@ def test_c1_reduce_sum_int_1mib_p2_host_buffers(mvx, oracle):
                       mvx.MPI_SUM, root)
         assert np.array_equal(R[root], ref[root])
     comm.free()
+
+
+@pytest.mark.parametrize("flavour", ["ch_shmem", "smp"])
+@pytest.mark.parametrize("where", ["device", "host"])
+@pytest.mark.parametrize("p", [2, 4])
+def test_successive_calls_do_not_interfere(mvx, comms, flavour, where, p):
+    """examples/test/coll/allred2.c (MPI_Allreduce of one int, alternating
+    +-10, checked after every call: 10 * size) and allredmany.c (MPI_Allreduce
+    of the double 10.0, repeated) -- back-to-back calls on one communicator
+    reuse its staging pool, so a stale slot would show here."""
+    import torch
+    comm = comms[p][flavour]
+
+    def bufs(vals, dt):
+        if where == "device":
+            return ([torch.tensor([v], dtype=dt, device="cuda") for v in vals],
+                    [torch.zeros(1, dtype=dt, device="cuda") for _ in vals])
+        npdt = np.int32 if dt == torch.int32 else np.float64
+        return [np.array([v], npdt) for v in vals], [np.zeros(1, npdt) for _ in vals]
+
+    for i in range(200):                                      # allred2.c, MAX_LOOP 1000
+        v = 10 if i & 1 else -10
+        s, r = bufs([v] * p, torch.int32)
+        rc, rcs = comm.allreduce_multi(s, r, 1, mvx.MPI_INT, mvx.MPI_SUM)
+        assert rc == 0 and rcs == [0] * p
+        for x in r:
+            got = int(x.cpu()[0]) if where == "device" else int(x[0])
+            assert got == v * p, (i, got)
+    s, r = bufs([10.0] * p, torch.float64)
+    for i in range(200):                                      # allredmany.c, 10000 calls
+        rc, rcs = comm.allreduce_multi(s, r, 1, mvx.MPI_DOUBLE, mvx.MPI_SUM)
+        assert rc == 0
+    for x in r:
+        got = float(x.cpu()[0]) if where == "device" else float(x[0])
+        assert got == 10.0 * p
