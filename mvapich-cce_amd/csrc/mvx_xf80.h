@@ -121,9 +121,75 @@ XF_FN xf80 round_pack(xf80 pads, uint32_t s, int e, u128 S)
     return with_bits(pads, r, (s << 15) | enc);
 }
 
+// a + b for two normal operands (integer bit set, exponent 1..0x7ffe) whose
+// exponents differ by at most 64, in 64-bit halves: the same value, rounding
+// and encoding as add()'s general path (whose 128-bit shifts dominate the
+// emulated add on the device), which handles everything else.  Returns false
+// when the operands are outside that case.
+XF_FN bool add_normal(xf80 a, xf80 b, xf80 *out)
+{
+    const uint32_t ea = a.se & 0x7fff, eb = b.se & 0x7fff;
+    if (ea - 1u >= 0x7ffeu || eb - 1u >= 0x7ffeu || !(a.m >> 63) || !(b.m >> 63)) return false;
+    uint32_t sa = a.se >> 15, sb = b.se >> 15;
+    int xa = (int)ea, xb = (int)eb;
+    uint64_t ma = a.m, mb = b.m;
+    if (xb > xa || (xb == xa && mb > ma)) {          // |a| >= |b| from here
+        const int t = xa; xa = xb; xb = t;
+        const uint64_t tm = ma; ma = mb; mb = tm;
+        const uint32_t ts = sa; sa = sb; sb = ts;
+    }
+    const int d = xa - xb;
+    if (d > 64) return false;
+    // B = mb * 2^(64 - d) as hi:lo below A = ma:0 (no bit is lost for d <= 64)
+    const uint64_t hi = d == 64 ? 0 : mb >> d;
+    const uint64_t lo = d == 0 ? 0 : (d == 64 ? mb : mb << (64 - d));
+    uint64_t rh, rl;
+    int e = xa;
+    if (sa == sb) {
+        rh = ma + hi;
+        rl = lo;
+        if (rh < ma) {                                // carry out: shift right, keep sticky
+            rl = (rh << 63) | (rl >> 1) | (rl & 1);
+            rh = (rh >> 1) | (1ull << 63);
+            ++e;
+        }
+    } else {
+        rl = 0 - lo;
+        rh = ma - hi - (lo != 0);
+        if (rh == 0 && rl == 0) {                     // exact cancellation: +0
+            *out = with_bits(a, 0, 0);
+            return true;
+        }
+        int lz = rh ? __builtin_clzll(rh) : 64 + __builtin_clzll(rl);
+        if (lz > e - 1) lz = e - 1;                   // a tiny result stays denormal
+        if (lz >= 64) {
+            rh = rl << (lz - 64);
+            rl = 0;
+        } else if (lz > 0) {
+            rh = (rh << lz) | (rl >> (64 - lz));
+            rl <<= lz;
+        }
+        e -= lz;
+    }
+    if ((rl >> 63) && ((rl << 1) || (rh & 1))) {      // round to nearest even
+        if (++rh == 0) {
+            rh = 1ull << 63;
+            ++e;
+        }
+    }
+    if (e >= 0x7fff) {
+        *out = with_bits(a, 1ull << 63, (sa << 15) | 0x7fff);   // overflow
+        return true;
+    }
+    *out = with_bits(a, rh, (sa << 15) | ((rh >> 63) ? (uint32_t)e : 0u));
+    return true;
+}
+
 // a + b (the reference's `a[i] = a[i] + b[i]`); pads from a
 XF_FN xf80 add(xf80 a, xf80 b)
 {
+    xf80 r;
+    if (add_normal(a, b, &r)) return r;
     const uint32_t ea = a.se & 0x7fff, eb = b.se & 0x7fff;
     uint32_t sa = a.se >> 15, sb = b.se >> 15;
     const int ka = klass(a.m, ea), kb = klass(b.m, eb);

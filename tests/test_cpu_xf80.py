@@ -74,3 +74,36 @@ def test_pattern_classes_present():
     assert ((e > 0) & (e < 0x7fff) & (j == 0)).any()                                     # unnormals
     assert ((e == 0x7fff) & (j == 0)).any()                                              # pseudo-inf/NaN
     assert ((e == 0x7fff) & (a["m"] == np.uint64(1 << 63))).any()                        # infinity
+
+
+def test_add_normal_operands_every_exponent_gap(oracle, xf_host):
+    """The 64-bit fast path of xf::add (normal operands, exponent gap <= 64)
+    against the x87: every gap 0..80 (beyond 64 the general path), both
+    signs, exponents at the denormal and overflow edges, significands with
+    long runs of ones / zeros (carries, borrows, ties at the rounding bit)."""
+    rng = np.random.default_rng(7)
+    n = 200000
+    dt = np.dtype([("m", "<u8"), ("se", "<u2"), ("p0", "<u2"), ("p1", "<u4")])
+    a = np.zeros(n, dt)
+    b = np.zeros(n, dt)
+    gap = rng.integers(0, 81, n)
+    base = rng.choice(np.array([1, 2, 3, 64, 65, 66, 100, 16383, 0x7ffe - 80, 0x7ffd, 0x7ffe]), n)
+    ea = np.clip(base + rng.integers(0, 3, n), 1, 0x7ffe)
+    eb = np.clip(ea - gap, 1, 0x7ffe)
+    swap = rng.random(n) < 0.5
+    ea, eb = np.where(swap, eb, ea), np.where(swap, ea, eb)
+    def sig(k):
+        m = rng.integers(0, 1 << 63, k, dtype=np.uint64) | np.uint64(1 << 63)
+        pick = rng.integers(0, 4, k)
+        m = np.where(pick == 0, np.uint64(0xFFFFFFFFFFFFFFFF), m)                  # all ones
+        m = np.where(pick == 1, np.uint64(1 << 63) | rng.integers(0, 4, k, dtype=np.uint64), m)
+        return m
+    a["m"], b["m"] = sig(n), sig(n)
+    a["se"] = (ea | (rng.integers(0, 2, n) << 15)).astype(np.uint16)
+    b["se"] = (eb | (rng.integers(0, 2, n) << 15)).astype(np.uint16)
+    a["p0"], a["p1"] = 0x1234, 0x89abcdef
+    ref, got = a.copy(), a.copy()
+    assert oracle.op(102, 12, b.view(np.uint8), ref.view(np.uint8), n) == 0
+    assert xf_host.xf_host_op(102, 12, b.ctypes.data, got.ctypes.data, n) == 0
+    msg = _first_diff(got, ref, b, a)
+    assert msg is None, msg
