@@ -254,7 +254,10 @@ def test_c4_full_size_reduce_scatter_band_int64_4x1gib(mvx, oracle, comms):
     _full_size(mvx, oracle, comms, "rs", 4, n, 8, 105, 2, cnts=[n // 4] * 4)
 
 
-def test_c5_full_size_allreduce_maxloc_float_int_8x64mi(mvx, oracle, comms):
+@pytest.mark.parametrize("dist", [3, 4])
+def test_c5_full_size_allreduce_maxloc_float_int_8x64mi(mvx, oracle, comms, dist):
     """Config 5 at full size: 8 ranks x 64 Mi MPI_FLOAT_INT pairs MPI_MAXLOC
-    with many ties (v = u % 1024, loc = rank*n + i), bit-exact."""
-    _full_size(mvx, oracle, comms, "ar", 8, 64 << 20, 17, 111, 4)
+    with many ties (v = u % 1024), bit-exact, on both SURVEY.md 8(d) index
+    choices: loc = rank (3, every tie is settled by the min-loc rule across
+    ranks) and loc = rank*n + i (4)."""
+    _full_size(mvx, oracle, comms, "ar", 8, 64 << 20, 17, 111, dist)

@@ -212,13 +212,16 @@ def test_integer_wrap(mvx, oracle):
             assert T.bytes_equal(T.from_dev(db), ref)
 
 
-def test_c2_headline_256mib_sum_f32(mvx, oracle):
-    """Config 2 at full size: 256 MiB MPI_SUM on MPI_FLOAT, bit-exact."""
+@pytest.mark.parametrize("dist", [0, 1])
+def test_c2_headline_256mib_sum_f32(mvx, oracle, dist):
+    """Config 2 at full size: 256 MiB MPI_SUM on MPI_FLOAT, bit-exact, on
+    both SURVEY.md 8(d) inputs: mixed sign with an exponent spread (0) and
+    U[0,1) (1)."""
     n = 64 * 1024 * 1024
     a = np.empty(n, np.float32)
     b = np.empty(n, np.float32)
-    oracle.fill(a, n, 0, 0)
-    oracle.fill(b, n, 0, 1)
+    oracle.fill(a, n, dist, 0)
+    oracle.fill(b, n, dist, 1)
     da, db = T.to_dev(a), T.to_dev(b)
     assert mvx.op_apply(102, 10, da, db, n) == 0
     oracle.op(102, 10, a.view(np.uint8), b.view(np.uint8), n)
