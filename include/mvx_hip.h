@@ -124,6 +124,17 @@ int mvx_type_unpack(int type, const void *packed, void *origin, size_t count, vo
 int mvx_op_apply(int op, int dtype, const void *in, void *inout, size_t n,
                  void *hip_stream);
 
+/* The Fortran .TRUE. / .FALSE. words MPI_LOGICAL's LAND / LOR / LXOR read
+ * and write: a = TO_FLOG(FROM_FLOG(a) op FROM_FLOG(b)), with
+ * FROM_FLOG(x) = (x == true_value) and TO_FLOG(v) = v ? true_value :
+ * false_value (src/fortran/include/mpi_fort.h:10-19, global_ops.c:646-655,
+ * 875-884, 1104-1113).  Replaces the reference's globals MPIR_F_TRUE /
+ * MPIR_F_FALSE, which mpir_init_flog sets from the Fortran compiler's
+ * literals (initfutil.c:100-102, 189).  The default is 1 / 0, gfortran's
+ * literals.  The values go to the current device; call this once per
+ * device, before launching. */
+int mvx_set_fortran_logical(int true_value, int false_value);
+
 /* dst[i] = shape-combine over leaves; leaf q = srcs[q][i] if fold == NULL or
  * fold[q] == NULL, else op(srcs[q][i], fold[q][i]) (srcs[q] is the inout
  * role).  srcs / fold are HOST arrays of k device pointers; 1 <= k <=

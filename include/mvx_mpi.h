@@ -54,8 +54,29 @@ typedef long MPI_Aint;      /* x86-64 LP64, the reference build's address int */
 #define MPI_SHORT_INT          ((MPI_Datatype)20)
 #define MPI_2INT               ((MPI_Datatype)21)
 #define MPI_LONG_DOUBLE_INT    ((MPI_Datatype)22)
+/* The Fortran types (mpi.h:101-113).  A Fortran-enabled build registers them
+ * in MPI_Init (initutil.c:421-422 -> MPIR_InitFortranDatatypes,
+ * src/fortran/src/initfutil.c:220-349), for C callers too.  The layout is
+ * x86-64 with gfortran: INTEGER / REAL / LOGICAL are 4 bytes,
+ * DOUBLE PRECISION is 8 bytes.
+ *   INTEGER, REAL, DOUBLE_PRECISION  the int / float / double kernels
+ *                                    (dte_type MPIR_INT / FLOAT / DOUBLE)
+ *   LOGICAL                          dte_type MPIR_LOGICAL (global_ops.c:646-655 ...)
+ *   2INTEGER / 2REAL / 2DOUBLE_PRECISION / 2COMPLEX / 2DOUBLE_COMPLEX
+ *                                    contiguous(2, INTEGER / FLOAT / DOUBLE /
+ *                                    COMPLEX / DOUBLE_COMPLEX) */
 #define MPI_COMPLEX            ((MPI_Datatype)23)
 #define MPI_DOUBLE_COMPLEX     ((MPI_Datatype)24)
+#define MPI_LOGICAL            ((MPI_Datatype)25)
+#define MPI_REAL               ((MPI_Datatype)26)
+#define MPI_DOUBLE_PRECISION   ((MPI_Datatype)27)
+#define MPI_INTEGER            ((MPI_Datatype)28)
+#define MPI_2INTEGER           ((MPI_Datatype)29)
+#define MPI_2COMPLEX           ((MPI_Datatype)30)
+#define MPI_2DOUBLE_COMPLEX    ((MPI_Datatype)31)
+#define MPI_2REAL              ((MPI_Datatype)32)
+#define MPI_2DOUBLE_PRECISION  ((MPI_Datatype)33)
+#define MPI_CHARACTER          ((MPI_Datatype)1)
 #define MPI_UNSIGNED_LONG_LONG ((MPI_Datatype)35)
 
 /* Ops: reference include/mpi.h:127-140 */

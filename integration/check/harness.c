@@ -147,6 +147,7 @@ int h_host_calls(void) { return g_host_calls; }
 #ifdef HARNESS_SMP
 int enable_shmem_collectives = 1;     /* src/env/initutil.c:146 */
 #endif
+MPI_Fint MPIR_F_TRUE = 1, MPIR_F_FALSE = 0;   /* initfutil.c:100, gfortran's literals */
 
 /* one-rank world, the shim's table installed */
 int h_init(void)

@@ -8,6 +8,7 @@ typedef int MPI_Datatype;                      /* mpi.h:29 */
 typedef int MPI_Comm;
 typedef int MPI_Op;
 typedef long MPI_Aint;                         /* mpidefs.h.in (@MPI_AINT@, long on LP64) */
+typedef int MPI_Fint;                          /* mpidefs.h.in:9 */
 
 #define MPI_SUCCESS        0                   /* mpi_errno.h:22 */
 #define MPI_ERR_TYPE       3                   /* :26 */

@@ -23,6 +23,7 @@
  *                             extent, size, lb, ub        mpid/ch2/datatype.h:26-56
  *   struct MPIR_OP            op, commute, permanent      include/mpiops.h:4-9
  *   MPIR_ToPointer, MPIR_GET_OP_PTR, MPIR_COMM_WORLD      include/mpiimpl.h:171-194
+ *   MPIR_F_TRUE, MPIR_F_FALSE (Fortran-enabled builds)    src/fortran/src/initfutil.c:100-102
  * and keeps its per-communicator state in an attribute (MPI_Keyval_create
  * with a delete callback, src/context/keyvalcreate.c:57), so MPI_Comm_free
  * releases the libmvx communicator.
@@ -68,6 +69,9 @@
 
 #ifdef _SMP_
 extern int enable_shmem_collectives;     /* src/env/initutil.c:146 */
+#endif
+#ifndef MPID_NO_FORTRAN
+extern MPI_Fint MPIR_F_TRUE, MPIR_F_FALSE;   /* src/fortran/src/initfutil.c:100-102 */
 #endif
 
 MPIR_COLLOPS MPIR_mvx_collops;           /* installed by MPIR_Comm_collops_init */
@@ -135,10 +139,16 @@ static int shim_comm(struct MPIR_COMMUNICATOR *comm)
     if (comm->local_rank == 0) mvx_get_unique_id(id);
     rc = MPIR_intra_collops->Bcast(id, MVX_UNIQUE_ID_BYTES, MPIR_GET_DTYPE_PTR(MPI_BYTE), 0, comm);
     if (rc != MPI_SUCCESS ||
-        mvx_comm_init(&s->mvx, comm->local_rank, comm->np, shim_device(), id) != 0)
+        mvx_comm_init(&s->mvx, comm->local_rank, comm->np, shim_device(), id) != 0) {
         s->mvx = -1;
-    else
+    } else {
         shim_tuning(s->mvx, comm);
+#ifndef MPID_NO_FORTRAN
+        /* MPI_LOGICAL's words, as mpir_init_flog set them (initfutil.c:189),
+           on the device mvx_comm_init made current */
+        mvx_set_fortran_logical(MPIR_F_TRUE, MPIR_F_FALSE);
+#endif
+    }
     MPI_Attr_put(comm->self, g_keyval, s);
     return s->mvx;
 }

@@ -127,6 +127,7 @@ def _load():
     _hip.mvx_hip_last_launch.argtypes = [ctypes.POINTER(ctypes.c_uint), ctypes.POINTER(ctypes.c_size_t),
                                          ctypes.POINTER(ctypes.c_int)]
     _hip.mvx_hip_last_launch.restype = None
+    _hip.mvx_set_fortran_logical.argtypes = [i, i]
     c = _coll
     c.mvx_get_unique_id.argtypes = [vp]
     c.mvx_comm_init.argtypes = [pi, i, i, i, vp]

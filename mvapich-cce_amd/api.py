@@ -13,6 +13,7 @@ __all__ = [
     "addr", "stream_handle", "op_apply", "op_combine", "op_program", "Comm",
     "MPI_Allreduce", "MPI_Reduce", "MPI_Reduce_scatter", "MPI_Scan", "MPI_Op_create", "MPI_Op_free", "op_create_device",
     "MPIR_call", "op_errno", "last_kernel", "last_kernel_symbol", "last_launch", "set_launch",
+    "set_fortran_logical",
     "MPI_Type_contiguous", "MPI_Type_commit", "MPI_Type_free", "MPI_Type_extent", "MPI_Type_size",
     "MPI_Type_vector", "MPI_Type_hvector", "MPI_Type_indexed", "MPI_Type_hindexed", "MPI_Type_struct",
     "MPI_Type_lb", "MPI_Type_ub", "type_layout", "type_set_handle", "type_pack", "type_unpack",
@@ -86,6 +87,12 @@ def last_launch():
     b, lds, occ = ctypes.c_uint(), ctypes.c_size_t(), ctypes.c_int()
     hip().mvx_hip_last_launch(ctypes.byref(b), ctypes.byref(lds), ctypes.byref(occ))
     return b.value, lds.value, occ.value
+
+
+def set_fortran_logical(true_value, false_value):
+    """MPI_LOGICAL's .TRUE. / .FALSE. words (mvx_set_fortran_logical; the
+    reference's MPIR_F_TRUE / MPIR_F_FALSE), on the current device."""
+    return hip().mvx_set_fortran_logical(true_value, false_value)
 
 
 # ------------------------------------------------------------- communicators

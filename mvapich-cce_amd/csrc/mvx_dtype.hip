@@ -89,6 +89,16 @@ static bool basic(int h, Type &t)
     case MPI_COMPLEX: base(8); t.align = 4; return true;
     case MPI_DOUBLE_COMPLEX: base(16); t.align = 8; return true;
     case MPI_2INT: base(8); t.align = 4; t.old = MPI_INT; t.count = 2; return true;   // contig(2, INT), :167
+    // the Fortran types (initfutil.c:238-323; gfortran: 4-byte INTEGER /
+    // REAL / LOGICAL, 8-byte DOUBLE PRECISION); the pairs are contiguous(2, x)
+    // over the old type initfutil.c names, with that type's alignment
+    case MPI_INTEGER: case MPI_REAL: case MPI_LOGICAL: base(4); return true;
+    case MPI_DOUBLE_PRECISION: base(8); return true;
+    case MPI_2INTEGER: base(8); t.align = 4; t.old = MPI_INTEGER; t.count = 2; return true;      // :323
+    case MPI_2REAL: base(8); t.align = 4; t.old = MPI_FLOAT; t.count = 2; return true;           // :263
+    case MPI_2DOUBLE_PRECISION: base(16); t.align = 8; t.old = MPI_DOUBLE; t.count = 2; return true;   // :286
+    case MPI_2COMPLEX: base(16); t.align = 4; t.old = MPI_COMPLEX; t.count = 2; return true;     // :318
+    case MPI_2DOUBLE_COMPLEX: base(32); t.align = 8; t.old = MPI_DOUBLE_COMPLEX; t.count = 2; return true;
     case MPI_FLOAT_INT: pair(4, 4, 8, 4, 1); return true;
     case MPI_DOUBLE_INT: pair(8, 8, 16, 8, 0); return true;
     case MPI_LONG_INT: pair(8, 8, 16, 8, 0); return true;
@@ -158,9 +168,11 @@ static int contiguous(int count, int oldtype, int *newtype)
         n.dense = 1;
         return store(n, newtype);
     }
-    // 139-146: a contiguous old type that has an old type itself (MPI_2INT,
-    // a derived contiguous type) is flattened to that old type
-    const bool has_old = oldtype == MPI_2INT || (slot(oldtype) && o->kind == K_CONTIG && !o->no_old);
+    // 139-146: a contiguous old type that has an old type itself (MPI_2INT
+    // and the Fortran pairs, which MPIR_Type_contiguous built; a derived
+    // contiguous type) is flattened to that old type
+    const bool has_old = (o->kind == K_BASIC && o->count == 2) ||
+                         (slot(oldtype) && o->kind == K_CONTIG && !o->no_old);
     const Type *ot = o;
     if (o->is_contig && has_old) {
         ot = get(o->old, iv);

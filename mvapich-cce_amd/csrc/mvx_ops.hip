@@ -190,6 +190,25 @@ __device__ __forceinline__ pp<xf80> xloc2(pp<xf80> a, pp<xf80> b)
 template <> struct F<OMAXLOC, pp<xf80>> { static __device__ __forceinline__ pp<xf80> f(pp<xf80> a, pp<xf80> b) { return xloc2<false>(a, b); } };
 template <> struct F<OMINLOC, pp<xf80>> { static __device__ __forceinline__ pp<xf80> f(pp<xf80> a, pp<xf80> b) { return xloc2<true>(a, b); } };
 
+// MPI_LOGICAL (dte_type MPIR_LOGICAL, one MPI_Fint): LAND / LOR / LXOR
+// compare each word with the Fortran .TRUE. and store .TRUE. or .FALSE.
+// (global_ops.c:646-655, 875-884, 1104-1113 with mpi_fort.h:11-19:
+// FROM_FLOG(x) = x == MPIR_F_TRUE, TO_FLOG(v) = v ? MPIR_F_TRUE :
+// MPIR_F_FALSE).  BAND / BOR / BXOR are bitwise on the word (678-684 ...)
+// and run the 32-bit integer kernels.
+struct flog { int32_t v; };
+__constant__ int32_t g_flog[2] = {1, 0};     // MPIR_F_TRUE, MPIR_F_FALSE (gfortran)
+__device__ __forceinline__ flog to_flog(bool t) { flog r; r.v = t ? g_flog[0] : g_flog[1]; return r; }
+template <> struct F<OLAND, flog> {
+    static __device__ __forceinline__ flog f(flog a, flog b) { return to_flog(a.v == g_flog[0] && b.v == g_flog[0]); }
+};
+template <> struct F<OLOR, flog> {
+    static __device__ __forceinline__ flog f(flog a, flog b) { return to_flog(a.v == g_flog[0] || b.v == g_flog[0]); }
+};
+template <> struct F<OLXOR, flog> {
+    static __device__ __forceinline__ flog f(flog a, flog b) { return to_flog((a.v == g_flog[0]) != (b.v == g_flog[0])); }
+};
+
 // ---------------------------------------------------------------------------
 // launch parameters (passed by value, ~170 bytes of kernarg)
 
@@ -675,7 +694,21 @@ enum { EK_NONE = 0, EK_I8, EK_U8, EK_BYTE, EK_I16, EK_U16, EK_I32, EK_U32,
        EK_I64, EK_U64, EK_F32, EK_F64, EK_C32, EK_C64, EK_PFI, EK_PDI, EK_PLI,
        EK_PSI, EK_PII, EK_LDBL, EK_LDBL_INT,
        // derived contiguous types: count-2 pairs of one base, and the rest
-       EK_PP8, EK_PP16, EK_PP64, EK_PPF, EK_PPD, EK_PPX, EK_DERIVED };
+       EK_PP8, EK_PP16, EK_PP64, EK_PPF, EK_PPD, EK_PPX, EK_DERIVED,
+       EK_LOGICAL };
+
+// a handle's dte_type, where the Fortran types share one with a C type
+// (initfutil.c:238-245, 261, 279: INTEGER is MPIR_INT, REAL MPIR_FLOAT,
+// DOUBLE PRECISION MPIR_DOUBLE); the old types of derived types switch on it
+static int dte_of(int h)
+{
+    switch (h) {
+    case MPI_INTEGER: return MPI_INT;
+    case MPI_REAL: return MPI_FLOAT;
+    case MPI_DOUBLE_PRECISION: return MPI_DOUBLE;
+    default: return h;
+    }
+}
 
 // the op kind of a derived handle (mvx_dtype.hip): MAXLOC / MINLOC are the
 // only ops with derived cases -- a count-2 contiguous type over one base
@@ -685,7 +718,7 @@ enum { EK_NONE = 0, EK_I8, EK_U8, EK_BYTE, EK_I16, EK_U16, EK_I32, EK_U32,
 static int derived_kind(const dt::Info &d)
 {
     if (d.kind == dt::K_STRUCT) {
-        switch (d.old) {
+        switch (dte_of(d.old)) {
         case MPI_INT: return EK_PII;             // MPIR_2int_loctype
         case MPI_FLOAT: return EK_PFI;
         case MPI_LONG: case MPI_LONG_LONG_INT: return EK_PLI;
@@ -696,7 +729,7 @@ static int derived_kind(const dt::Info &d)
         }
     }
     if (d.kind != dt::K_CONTIG || d.count != 2) return EK_DERIVED;
-    switch (d.old) {              // the base's dte_type, global_ops.c:1395-1497
+    switch (dte_of(d.old)) {      // the base's dte_type, global_ops.c:1395-1497
     case MPI_INT: return EK_PII;
     case MPI_LONG: case MPI_LONG_LONG_INT: return EK_PP64;
     case MPI_SHORT: return EK_PP16;
@@ -735,6 +768,16 @@ static int ekind(int dtype)
     case MPI_2INT: return EK_PII;
     case MPI_LONG_DOUBLE: return EK_LDBL;
     case MPI_LONG_DOUBLE_INT: return EK_LDBL_INT;
+    case MPI_INTEGER: return EK_I32;
+    case MPI_REAL: return EK_F32;
+    case MPI_DOUBLE_PRECISION: return EK_F64;
+    case MPI_LOGICAL: return EK_LOGICAL;
+    // the Fortran pairs: contiguous(2, x), the MAXLOC / MINLOC stride-2 case
+    // of x's dte_type (global_ops.c:1387-1503); no case for COMPLEX (1498)
+    case MPI_2INTEGER: return EK_PII;
+    case MPI_2REAL: return EK_PPF;
+    case MPI_2DOUBLE_PRECISION: return EK_PPD;
+    case MPI_2COMPLEX: case MPI_2DOUBLE_COMPLEX: return EK_DERIVED;
     default: return EK_NONE;
     }
 }
@@ -773,6 +816,8 @@ static int ekind(int dtype)
     case EK_LDBL: { static KSet s = kset<O, xf80>(NAME "_f80"); return &s; }
 #define LDBL_INT(O, NAME)                                                    \
     case EK_LDBL_INT: { static KSet s = kset<O, pxi>(NAME "_long_double_int"); return &s; }
+#define LOGICAL(O, NAME)                                                     \
+    case EK_LOGICAL: { static KSet s = kset<O, flog>(NAME "_logical"); return &s; }
 #define CONTIG_PAIRS(O, NAME)                                                \
     case EK_PP8:  { static KSet s = kset<O, pp<int8_t>>(NAME "_2char"); return &s; } \
     case EK_PP16: { static KSet s = kset<O, pp<int16_t>>(NAME "_2short"); return &s; } \
@@ -787,8 +832,11 @@ static int ekind(int dtype)
 // handle outside MPI_MAX..MPI_MAXLOC.
 static const KSet *lookup(int op, int dtype, int *rc)
 {
-    const int ek = ekind(dtype);
+    int ek = ekind(dtype);
     *rc = MVX_ERR_OP_NOT_DEFINED;
+    if (ek == EK_LOGICAL && (op == MPI_BAND || op == MPI_BOR || op == MPI_BXOR))
+        ek = EK_U32;                 // bitwise on the MPI_Fint word
+
     switch (op) {
     case MPI_MAX:
         switch (ek) { SIGNED_INT(OMAX, "max") FLOATS(OMAX, "max")
@@ -804,13 +852,13 @@ static const KSet *lookup(int op, int dtype, int *rc)
         LDBL(OPROD, "prod") default: return nullptr; }
     case MPI_LAND:
         switch (ek) { ARITH_INT(OLAND, "land") FLOATS(OLAND, "land")
-        LDBL(OLAND, "land") default: return nullptr; }
+        LDBL(OLAND, "land") LOGICAL(OLAND, "land") default: return nullptr; }
     case MPI_LOR:
         switch (ek) { ARITH_INT(OLOR, "lor") FLOATS(OLOR, "lor")
-        LDBL(OLOR, "lor") default: return nullptr; }
+        LDBL(OLOR, "lor") LOGICAL(OLOR, "lor") default: return nullptr; }
     case MPI_LXOR:
         switch (ek) { ARITH_INT(OLXOR, "lxor") FLOATS(OLXOR, "lxor")
-        LDBL(OLXOR, "lxor") default: return nullptr; }
+        LDBL(OLXOR, "lxor") LOGICAL(OLXOR, "lxor") default: return nullptr; }
     case MPI_BAND:
         switch (ek) { case EK_BYTE: ARITH_INT(OBAND, "band") default: return nullptr; }
     case MPI_BOR:
@@ -947,6 +995,12 @@ static int launch(const KSet *ks, const KFam &F, Params &P, hipStream_t stream)
 }  // namespace mvx
 
 using namespace mvx;
+
+extern "C" int mvx_set_fortran_logical(int true_value, int false_value)
+{
+    const int32_t v[2] = {true_value, false_value};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_flog), v, sizeof v) == hipSuccess ? MPI_SUCCESS : MPI_ERR_OTHER;
+}
 
 extern "C" int mvx_op_supported(int op, int dtype)
 {

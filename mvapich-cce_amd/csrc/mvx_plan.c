@@ -159,23 +159,29 @@ int mvx_plan_algorithm_tuned(int coll, int p, long total, int dtype, int kind,
  * global_ops.c:1297-1309), and for every op on the x87 types: an x87 store
  * writes 10 bytes, so the 6 padding bytes of the 16-byte slot, which
  * MPI_LONG_DOUBLE's type map moves, stay those of the inout operand. */
+static int is_ieee(int t)
+{
+    return t == MPI_FLOAT || t == MPI_DOUBLE || t == MPI_LONG_DOUBLE || t == MPI_REAL ||
+           t == MPI_DOUBLE_PRECISION;
+}
+
 static int op_symmetric(int op, int dtype)
 {
     int old = dtype, cnt = 1;
     if (dtype == MPI_LONG_DOUBLE || dtype == MPI_LONG_DOUBLE_INT) return 0;
-    if (dtype >= MVX_TYPE_DERIVED_BASE) {
+    if (dtype >= MVX_TYPE_DERIVED_BASE || dtype == MPI_2REAL || dtype == MPI_2DOUBLE_PRECISION) {
         /* count-2 contiguous {value, loc} pairs of one base type: the IEEE /
          * x87 ones pick operands by role (NaN, +-0, slot padding) */
         mvx_type_describe(dtype, &old, &cnt, NULL, NULL);
         if (op != MPI_MAXLOC && op != MPI_MINLOC) return 0;
-        return !(old == MPI_FLOAT || old == MPI_DOUBLE || old == MPI_LONG_DOUBLE);
+        return !is_ieee(old);
     }
     switch (op) {
     case MPI_SUM: case MPI_PROD: case MPI_LAND: case MPI_LOR: case MPI_LXOR:
     case MPI_BAND: case MPI_BOR: case MPI_BXOR:
         return 1;
     case MPI_MAX: case MPI_MIN:
-        return !(dtype == MPI_FLOAT || dtype == MPI_DOUBLE || dtype == MPI_LONG_DOUBLE);
+        return !is_ieee(dtype);
     case MPI_MAXLOC: case MPI_MINLOC:
         return !(dtype == MPI_FLOAT_INT || dtype == MPI_DOUBLE_INT ||
                  dtype == MPI_LONG_DOUBLE_INT);

@@ -18,6 +18,9 @@
  *   BXOR a = a ^ b                    global_ops.c:1124-1226
  *   MAXLOC/MINLOC on struct pair types (global_ops.c:1271-1384,1511-1620)
  *   and on the contiguous MPI_2INT (global_ops.c:1387-1503, 1622-1740).
+ *   The Fortran types of a Fortran-enabled build: INTEGER / REAL / DOUBLE
+ *   PRECISION as int / float / double, LOGICAL (646-655 and siblings), and
+ *   the contiguous pairs 2INTEGER / 2REAL / 2DOUBLE_PRECISION.
  * The C element types are the reference's (char is signed on x86-64, long is
  * 64-bit, long double is x87 80-bit in a 16-byte slot), compiled by the same
  * gcc at -O2; -fwrapv makes the signed wrap the reference gets in practice
@@ -35,7 +38,26 @@
 enum { T_CHAR = 1, T_UCHAR, T_BYTE, T_SHORT, T_USHORT, T_INT, T_UINT, T_LONG,
        T_ULONG, T_FLOAT, T_DOUBLE, T_LDOUBLE, T_LLONG, T_PACKED, T_LB, T_UB,
        T_FLOAT_INT, T_DOUBLE_INT, T_LONG_INT, T_SHORT_INT, T_2INT,
-       T_LDOUBLE_INT, T_COMPLEX, T_DCOMPLEX };
+       T_LDOUBLE_INT, T_COMPLEX, T_DCOMPLEX,
+       /* the Fortran types (mpi.h:104-112; initfutil.c:220-349) */
+       T_LOGICAL, T_REAL, T_DPREC, T_INTEGER, T_2INTEGER, T_2COMPLEX,
+       T_2DCOMPLEX, T_2REAL, T_2DPREC };
+
+/* MPIR_F_TRUE / MPIR_F_FALSE (initfutil.c:100-102; gfortran's literals) */
+static int g_ftrue = 1, g_ffalse = 0;
+
+void orc_set_flog(int true_value, int false_value)
+{
+    g_ftrue = true_value;
+    g_ffalse = false_value;
+}
+
+/* the dte_type a Fortran handle shares with a C type (initfutil.c:238-245,
+   261, 279; sizeof(int) == sizeof(float) == 4 with gfortran) */
+static int fdte(int t)
+{
+    return t == T_INTEGER ? T_INT : t == T_REAL ? T_FLOAT : t == T_DPREC ? T_DOUBLE : t;
+}
 
 typedef struct { float re, im; } s_cplx;
 typedef struct { double re, im; } d_cplx;
@@ -80,6 +102,10 @@ int orc_dtype_info(int dtype, int *extent, int *type_size)
        Fortran-enabled builds.  We accept them. */
     case T_COMPLEX: e = s = 8; break;
     case T_DCOMPLEX: e = s = 16; break;
+    case T_LOGICAL: case T_REAL: case T_INTEGER: e = s = 4; break;
+    case T_DPREC: case T_2INTEGER: case T_2REAL: e = s = 8; break;
+    case T_2DPREC: case T_2COMPLEX: e = s = 16; break;
+    case T_2DCOMPLEX: e = s = 32; break;
     default: return ERR_TYPE;
     }
     if (extent) *extent = e;
@@ -136,16 +162,36 @@ int orc_dtype_info(int dtype, int *extent, int *type_size)
         }                                                                    \
     } while (0)
 
+/* MAXLOC / MINLOC on a derived contiguous type with count == 2: stride-2
+ * scalars of the old type (global_ops.c:1387-1503, 1625-1740); len is
+ * doubled (1392).  Any other derived type: 329 (1504-1507, 1741-1744). */
+#define CONTIG2_LOOP(T)                                                      \
+    do {                                                                     \
+        T *a = (T *)inout; const T *b = (const T *)in;                       \
+        for (i = 0; i < n2; i += 2) {                                        \
+            if (a[i] == b[i])                                                \
+                a[i + 1] = (a[i + 1] > b[i + 1]) ? b[i + 1] : a[i + 1];      \
+            else if (is_min ? (a[i] > b[i]) : (a[i] < b[i])) {               \
+                a[i] = b[i];                                                 \
+                a[i + 1] = b[i + 1];                                         \
+            }                                                                \
+        }                                                                    \
+    } while (0)
+
 static int loc_op(int is_min, int dtype, const void *in, void *inout, int len)
 {
-    int i;
+    int i, n2 = len * 2;
     switch (dtype) {
     case T_FLOAT_INT:   PAIR_LOOP(p_float_int); return 0;
     case T_DOUBLE_INT:  PAIR_LOOP(p_double_int); return 0;
     case T_LONG_INT:    PAIR_LOOP(p_long_int); return 0;
     case T_SHORT_INT:   PAIR_LOOP(p_short_int); return 0;
     case T_LDOUBLE_INT: PAIR_LOOP(p_ldouble_int); return 0;
-    case T_2INT: {
+    /* the Fortran pairs: contiguous(2, REAL / DOUBLE PRECISION) run the
+       stride-2 case of their old type's dte_type (1459-1482) */
+    case T_2REAL:  CONTIG2_LOOP(float); return 0;
+    case T_2DPREC: CONTIG2_LOOP(double); return 0;
+    case T_2INT: case T_2INTEGER: {
         /* contiguous count-2 type: stride-2 scalars (global_ops.c:1387-1403) */
         int *a = (int *)inout; const int *b = (const int *)in;
         int n2 = len * 2;
@@ -164,22 +210,6 @@ static int loc_op(int is_min, int dtype, const void *in, void *inout, int len)
     }
 }
 
-/* MAXLOC / MINLOC on a derived contiguous type with count == 2: stride-2
- * scalars of the old type (global_ops.c:1387-1503, 1625-1740); len is
- * doubled (1392).  Any other derived type: 329 (1504-1507, 1741-1744). */
-#define CONTIG2_LOOP(T)                                                      \
-    do {                                                                     \
-        T *a = (T *)inout; const T *b = (const T *)in;                       \
-        for (i = 0; i < n2; i += 2) {                                        \
-            if (a[i] == b[i])                                                \
-                a[i + 1] = (a[i + 1] > b[i + 1]) ? b[i + 1] : a[i + 1];      \
-            else if (is_min ? (a[i] > b[i]) : (a[i] < b[i])) {               \
-                a[i] = b[i];                                                 \
-                a[i + 1] = b[i + 1];                                         \
-            }                                                                \
-        }                                                                    \
-    } while (0)
-
 static int derived_loc_op(int is_min, int dtype, const void *in, void *inout, int len)
 {
     int old, count, i, n2, kind;
@@ -187,7 +217,7 @@ static int derived_loc_op(int is_min, int dtype, const void *in, void *inout, in
     if (kind == 4) {
         /* MPIR_STRUCT: the C pair struct of old_types[0]'s dte_type
          * (global_ops.c:1280-1384, 1520-1620) */
-        switch (old) {
+        switch (fdte(old)) {
         case T_INT: return loc_op(is_min, T_2INT, in, inout, len);    /* MPIR_2int_loctype */
         case T_FLOAT: return loc_op(is_min, T_FLOAT_INT, in, inout, len);
         case T_LONG: case T_LLONG: return loc_op(is_min, T_LONG_INT, in, inout, len);
@@ -199,7 +229,7 @@ static int derived_loc_op(int is_min, int dtype, const void *in, void *inout, in
     }
     if (kind != 1 || count != 2) return ERR_OP_NOT_DEFINED;
     n2 = len * count;
-    switch (old) {
+    switch (fdte(old)) {
     case T_INT:     CONTIG2_LOOP(int); return 0;
     case T_LONG:    CONTIG2_LOOP(long); return 0;
     case T_LLONG:   CONTIG2_LOOP(long long); return 0;
@@ -220,6 +250,30 @@ int orc_op(int op, int dtype, const void *in, void *inout, int len)
         if (op == 111 || op == 110) return derived_loc_op(op == 110, dtype, in, inout, len);
         return ERR_OP_NOT_DEFINED;   /* no MPIR_CONTIG case in any other op */
     }
+    if (dtype == T_LOGICAL) {
+        /* MPIR_LOGICAL, one MPI_Fint: the logical ops through FROM_FLOG /
+           TO_FLOG (global_ops.c:646-655, 875-884, 1104-1113; mpi_fort.h:11-19),
+           the bitwise ops on the word (678-684, 906-912, 1136-1142) */
+#define FROM_FLOG(x) ((x) == g_ftrue ? 1 : 0)
+#define TO_FLOG(v) ((v) ? g_ftrue : g_ffalse)
+        int *a = (int *)inout; const int *b = (const int *)in;
+        switch (op) {
+        case 104: for (i = 0; i < len; i++) a[i] = TO_FLOG(FROM_FLOG(a[i]) && FROM_FLOG(b[i])); return 0;
+        case 106: for (i = 0; i < len; i++) a[i] = TO_FLOG(FROM_FLOG(a[i]) || FROM_FLOG(b[i])); return 0;
+        case 108: for (i = 0; i < len; i++) {
+                      int x = FROM_FLOG(a[i]), y = FROM_FLOG(b[i]);
+                      a[i] = TO_FLOG((x && !y) || (!x && y));
+                  }
+                  return 0;
+        case 105: for (i = 0; i < len; i++) a[i] = a[i] & b[i]; return 0;
+        case 107: for (i = 0; i < len; i++) a[i] = a[i] | b[i]; return 0;
+        case 109: for (i = 0; i < len; i++) a[i] = a[i] ^ b[i]; return 0;
+        default: return (op < 100 || op > 111) ? ERR_OP : ERR_OP_NOT_DEFINED;
+        }
+#undef FROM_FLOG
+#undef TO_FLOG
+    }
+    if (op != 111 && op != 110) dtype = fdte(dtype);
     switch (op) {
     case 100: /* MPI_MAX */
         switch (dtype) { INT_CASES(E_MAX) FLT_CASES(E_MAX)

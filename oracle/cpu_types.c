@@ -69,6 +69,12 @@ static int basic(int h, dtype_t *t, long *off2, long *len2)
     case 21: t->align = 4; t->old = 6; t->count = 2; break;            /* 2INT = contig(2, INT) */
     case 23: t->align = 4; break;
     case 24: t->align = 8; break;
+    /* the Fortran pairs, contiguous(2, old) (initfutil.c:263, 286, 318-323) */
+    case 29: t->align = 4; t->old = 28; t->count = 2; break;           /* 2INTEGER */
+    case 30: t->align = 4; t->old = 23; t->count = 2; break;           /* 2COMPLEX */
+    case 31: t->align = 8; t->old = 24; t->count = 2; break;           /* 2DOUBLE_COMPLEX */
+    case 32: t->align = 4; t->old = 10; t->count = 2; break;           /* 2REAL */
+    case 33: t->align = 8; t->old = 11; t->count = 2; break;           /* 2DOUBLE_PRECISION */
     default: break;
     }
     return 0;
@@ -135,7 +141,9 @@ int orc_type_contiguous(int count, int oldtype, int *newtype)
         n.old = oldtype; n.is_contig = 1; n.align = 4;
         return store(&n, newtype);
     }
-    has_old = oldtype == 21 || (derived(oldtype) && o->kind == KC && !o->no_old);
+    /* MPI_2INT and the Fortran pairs have an old type, as derived contiguous
+       types do */
+    has_old = (o->kind == KB && o->count == 2) || (derived(oldtype) && o->kind == KC && !o->no_old);
     if (o->is_contig && has_old) {  /* 139-142 */
         ot = get(o->old, &w);
         n.old = o->old; n.count = count * o->count; n.is_contig = 1;

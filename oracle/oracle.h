@@ -64,6 +64,8 @@ int orc_type_block(int dtype, long i, long *off, long *len);
  * Returns 0, or 329 (MPIR_ERR_OP_NOT_DEFINED) for an undefined (op, type)
  * pair (the data is left untouched), or 9 (MPI_ERR_OP) for a bad handle. */
 int orc_op(int op, int dtype, const void *in, void *inout, int len);
+/* MPIR_F_TRUE / MPIR_F_FALSE for MPI_LOGICAL (default 1 / 0, gfortran) */
+void orc_set_flog(int true_value, int false_value);
 
 /* Collectives over p simulated ranks.  send[r]/recv[r] are rank r's
  * buffers; rc[r] receives rank r's return code.  Returns 0. */

@@ -35,6 +35,8 @@ def lib():
         vp = ctypes.c_void_p
         L.orc_dtype_info.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
         L.orc_op.argtypes = [ctypes.c_int, ctypes.c_int, vp, vp, ctypes.c_int]
+        L.orc_set_flog.argtypes = [ctypes.c_int, ctypes.c_int]
+        L.orc_set_flog.restype = None
         L.orc_call.argtypes = [ctypes.c_int, ctypes.c_int, vp, vp, ctypes.c_int]
         L.orc_allreduce.argtypes = [ctypes.c_int, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.c_int,
                                     ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
@@ -86,6 +88,11 @@ def op(op_handle, dtype, invec, inoutvec, count):
     """inoutvec = invec op inoutvec (in place, numpy uint8 views). Returns rc.
     User op handles (user_op_set) call the registered function."""
     return lib().orc_call(op_handle, dtype, _ptr(invec), _ptr(inoutvec), count)
+
+
+def set_fortran_logical(true_value, false_value):
+    """MPIR_F_TRUE / MPIR_F_FALSE of MPI_LOGICAL (default 1 / 0)."""
+    lib().orc_set_flog(true_value, false_value)
 
 
 def _ptrs(bufs):

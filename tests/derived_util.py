@@ -10,7 +10,8 @@ import mvxtest as T
 
 # base handle -> numpy scalar type of a {value, loc} stride-2 pair
 PAIR_BASES = {1: np.int8, 4: np.int16, 6: np.int32, 8: np.int64, 13: np.int64, 10: np.float32,
-              11: np.float64, 12: np.longdouble}
+              11: np.float64, 12: np.longdouble,
+              28: np.int32, 26: np.float32, 27: np.float64}    # MPI_INTEGER / REAL / DOUBLE_PRECISION
 
 
 def make_both(mvx, oracle, count, old):

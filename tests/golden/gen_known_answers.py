@@ -12,6 +12,8 @@ reduced to data (inputs per rank + the value the reference test asserts):
   examples/test/pt2pt/gcomm.c:24-50 adds the reversed, cartesian (4) and
   odd/even-split (2) communicators) -- and stores the numbers.  (Some
   answers are size-specific, e.g. LXOR of all-ones is 0 only for even p.)
+* allredf.f -- the Fortran types (MPI_INTEGER, REAL, DOUBLE_PRECISION,
+  COMPLEX, LOGICAL, 2INTEGER, 2REAL, 2DOUBLE_PRECISION), from its closed forms.
 * redscat.c (Reduce_scatter SUM INT, recvcounts 1), coll12.c (Reduce MAXLOC /
   Allreduce MINLOC on DOUBLE_INT, TABLE_SIZE 2), redtst.c (BOR: 3|6 == 7),
   shortint.c (Reduce MINLOC SHORT_INT, root 1), scantst.c / coll11.c (Scan SUM
@@ -71,6 +73,51 @@ def gen_c(cases):
         out.append("(void)out; } }")
     out.append("return 0; }")
     return "\n".join(out)
+
+
+def allredf_cases():
+    """examples/test/coll/allredf.f: the Fortran twin of allred.c, MPI_Allreduce
+    on MPI_INTEGER / REAL / DOUBLE_PRECISION / COMPLEX / LOGICAL / 2INTEGER /
+    2REAL / 2DOUBLE_PRECISION, count 10, i = 1..10.  Its init and solution
+    loops are closed forms of (i, rank, size), written out here.  LOGICAL
+    words are gfortran's .TRUE. = 1 / .FALSE. = 0 (the MPIR_F_TRUE /
+    MPIR_F_FALSE a gfortran build gets); COMPLEX values are [re, im]."""
+    out = []
+    I = range(1, COUNT + 1)
+
+    def case(t, o, size, fin, fsol, tag=""):
+        out.append({"test": "allredf.f" + tag, "coll": "allreduce", "type": t, "op": o, "size": size,
+                    "count": COUNT, "inputs": [[fin(r, i) for i in I] for r in range(size)],
+                    "expected": [[fsol(i) for i in I]] * size})
+
+    for size in SIZES:
+        for t in ("MPI_INTEGER", "MPI_REAL", "MPI_DOUBLE_PRECISION", "MPI_COMPLEX"):
+            cx = t == "MPI_COMPLEX"
+            val = (lambda x: [x, 0]) if cx else (lambda x: x)
+            case(t, "MPI_SUM", size, lambda r, i: val(i), lambda i: val(i * size))
+            case(t, "MPI_PROD", size, lambda r, i: val(i), lambda i: val(i ** size))
+        for t in ("MPI_INTEGER", "MPI_REAL", "MPI_DOUBLE_PRECISION"):
+            case(t, "MPI_MAX", size, lambda r, i: r + i, lambda i: size - 1 + i)
+            case(t, "MPI_MIN", size, lambda r, i: r + i, lambda i: i)
+        L = "MPI_LOGICAL"
+        case(L, "MPI_LOR", size, lambda r, i: int(r % 2 == 1), lambda i: int(size > 1), "(0)")
+        case(L, "MPI_LOR", size, lambda r, i: 0, lambda i: 0, "(1)")
+        case(L, "MPI_LXOR", size, lambda r, i: int(r == 1), lambda i: int(size > 1), "(0)")
+        case(L, "MPI_LXOR", size, lambda r, i: 0, lambda i: 0, "(1)")
+        case(L, "MPI_LXOR", size, lambda r, i: 1, lambda i: int(size % 2 != 0), "(2)")
+        case(L, "MPI_LAND", size, lambda r, i: int(r % 2 == 1), lambda i: 0, "(0)")
+        case(L, "MPI_LAND", size, lambda r, i: 1, lambda i: 1, "(1)")
+        N = "MPI_INTEGER"
+        case(N, "MPI_BOR", size, lambda r, i: r % 4, lambda i: size - 1 if size < 3 else 3)
+        case(N, "MPI_BAND", size, lambda r, i: i if r == size - 1 else -1, lambda i: i, "(1)")
+        case(N, "MPI_BAND", size, lambda r, i: i if r == size - 1 else 0, lambda i: 0, "(0)")
+        case(N, "MPI_BXOR", size, lambda r, i: 240 if r == 1 else 0, lambda i: 240 if size > 1 else 0, "(1)")
+        case(N, "MPI_BXOR", size, lambda r, i: 0, lambda i: 0, "(0)")
+        case(N, "MPI_BXOR", size, lambda r, i: -1, lambda i: 0 if size % 2 == 0 else -1, "(1-0)")
+        for t in ("MPI_2INTEGER", "MPI_2REAL", "MPI_2DOUBLE_PRECISION"):
+            case(t, "MPI_MAXLOC", size, lambda r, i: [r + i, r], lambda i: [size - 1 + i, size - 1])
+            case(t, "MPI_MINLOC", size, lambda r, i: [r + i, r], lambda i: [i, 0])
+    return out
 
 
 def num(tok, is_float):
@@ -152,8 +199,10 @@ def main():
                       "count": 1, "inputs": [[r] for r in range(size)],
                       "expected": [[r * (r + 1) // 2] for r in range(size)]})
 
+    extra += allredf_cases()
+
     doc = {"generated_by": "tests/golden/gen_known_answers.py",
-           "source": "reference examples/test/coll/{allred,redscat,coll12,redtst,shortint,scantst}.c",
+           "source": "reference examples/test/coll/{allred,redscat,coll12,redtst,shortint,scantst}.c, allredf.f",
            "allred": {"count": COUNT, "sizes": list(SIZES), "cases": cases},
            "other": extra}
     with open(OUT, "w") as f:

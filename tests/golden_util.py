@@ -33,6 +33,8 @@ def to_array(values, type_name):
     if dt.names:
         a["v"] = [v[0] for v in values]
         a["l"] = [v[1] for v in values]
+    elif dt.kind == "c":   # [re, im]
+        a[:] = [complex(v[0], v[1]) for v in values]
     elif dt.kind == "u":   # the generator prints unsigned values as long long
         a[:] = [int(v) % (1 << (8 * dt.itemsize)) for v in values]
     else:

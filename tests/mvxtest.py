@@ -2,11 +2,13 @@
 import numpy as np
 
 MPI_FLOAT, MPI_DOUBLE = 10, 11
-PAIRS = (17, 18, 19, 20, 21, 22)
+PAIRS = (17, 18, 19, 20, 21, 22, 29, 32, 33)
 ALL_OPS = list(range(100, 112))
 # every handle the device path knows, plus one unregistered-on-device (BYTE is
 # only valid for B* ops) and the two x87 long double types
-ALL_TYPES = [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 17, 18, 19, 20, 21, 22, 23, 24]
+# and the Fortran types 25-33
+ALL_TYPES = [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 17, 18, 19, 20, 21, 22, 23, 24,
+             25, 26, 27, 28, 29, 30, 31, 32, 33]
 
 _np_cache = {}
 
@@ -24,6 +26,8 @@ def rand_vec(dtype, n, seed):
     dt = np_dtype(dtype)
     if dtype == 12:
         return xf_rand(n, rng).view(np.longdouble)
+    if dtype == 25:     # MPI_LOGICAL: .TRUE. (1), .FALSE. (0) and other words
+        return rng.choice(np.array([0, 1, 1, 0, 2, -1, 1, 0], np.int32), n)
     if dtype == 22:
         out = np.zeros(n, dt)
         u = out.view(np.uint8).reshape(n, 32)
@@ -37,15 +41,13 @@ def rand_vec(dtype, n, seed):
         out["v"] = _rand_scalar(vt, n, rng)
         out["l"] = rng.integers(-5, 50, n)
         return out
-    if dt.kind == "c":
-        ft = np.float32 if dt.itemsize == 8 else np.float64
-        re = _rand_scalar(np.dtype(ft), n, rng)
-        im = _rand_scalar(np.dtype(ft), n, rng)
-        return (re + 1j * im).astype(dt)
     return _rand_scalar(dt, n, rng)
 
 
 def _rand_scalar(dt, n, rng):
+    if dt.kind == "c":
+        ft = np.dtype(np.float32 if dt.itemsize == 8 else np.float64)
+        return (_rand_scalar(ft, n, rng) + 1j * _rand_scalar(ft, n, rng)).astype(dt)
     if dt.kind == "f":
         v = rng.standard_normal(n) * np.exp2(rng.integers(-20, 20, n))
         v = np.where(rng.random(n) < 0.25, rng.integers(-3, 4, n), v)   # ties and zeros

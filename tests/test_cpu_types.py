@@ -86,7 +86,8 @@ def test_reference_type_known_answers(mvx, oracle, case):
 
 
 BASICS = ["MPI_INT", "MPI_CHAR", "MPI_DOUBLE", "MPI_FLOAT", "MPI_SHORT", "MPI_LONG", "MPI_DOUBLE_INT",
-          "MPI_FLOAT_INT", "MPI_SHORT_INT", "MPI_2INT", "MPI_BYTE", "MPI_LONG_DOUBLE"]
+          "MPI_FLOAT_INT", "MPI_SHORT_INT", "MPI_2INT", "MPI_BYTE", "MPI_LONG_DOUBLE",
+          "MPI_REAL", "MPI_LOGICAL", "MPI_2INTEGER", "MPI_2REAL", "MPI_2DOUBLE_COMPLEX"]
 
 
 def _random_step(rng, pool):

@@ -252,3 +252,32 @@ def test_x87_long_double_fuzz(mvx, oracle, op, dtype):
     bad = np.nonzero((g != r).any(1))[0]
     assert bad.size == 0, "%d differ; first %d: got %s ref %s" % (bad.size, bad[0], g[bad[0]].tobytes().hex(),
                                                                  r[bad[0]].tobytes().hex())
+
+
+@pytest.mark.parametrize("flog", [(-1, 0), (7, 3)])
+def test_logical_with_other_fortran_literals(mvx, oracle, flog):
+    """MPI_LOGICAL under another compiler's .TRUE. / .FALSE. words
+    (mvx_set_fortran_logical, the reference's MPIR_F_TRUE / MPIR_F_FALSE):
+    the op and an 8-leaf combine against the oracle with the same words."""
+    from plan_exec import combine_cpu
+    n = 70001
+    words = np.array([flog[0], flog[1], 0, 1, -1, 2], np.int32)
+    rng = np.random.default_rng(3)
+    try:
+        assert mvx.set_fortran_logical(*flog) == 0
+        oracle.set_fortran_logical(*flog)
+        for op in (104, 106, 108):
+            a, b = rng.choice(words, n), rng.choice(words, n)
+            db = T.to_dev(b)
+            assert mvx.op_apply(op, 25, T.to_dev(a), db, n) == 0
+            ref = T.clone(b)
+            oracle.op(op, 25, a.view(np.uint8), ref.view(np.uint8), n)
+            assert T.bytes_equal(T.from_dev(db), ref), op
+            leaves = [rng.choice(words, n) for _ in range(8)]
+            dst = T.to_dev(np.zeros(n, np.int32))
+            assert mvx.op_combine(op, 25, [T.to_dev(x) for x in leaves], dst, n, shape=0) == 0
+            ref = combine_cpu(op, 25, 4, [x.view(np.uint8) for x in leaves], [None] * 8, 0, n)
+            assert T.bytes_equal(T.from_dev(dst), ref), op
+    finally:
+        mvx.set_fortran_logical(1, 0)
+        oracle.set_fortran_logical(1, 0)
