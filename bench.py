@@ -318,6 +318,40 @@ def reference_run(cfg, world, n, dev, want_time):
     return digests, secs, reps
 
 
+def phase_breakdown(comm, step, coll, world, nbytes, reps=3):
+    """Untimed, after the timed region: `reps` more steps with HIP events
+    around phase A (exchange), B (combine) and C (distribution) on the launch
+    stream (mvx_comm_set_phase_timing); the median of each, MAX over ranks,
+    with the rate each phase reached: A / C as bytes each rank sends over
+    xGMI per ms, B as the combine's HBM bytes."""
+    import torch
+    import torch.distributed as dist
+    comm.set_phase_timing(True)
+    got = []
+    for _ in range(reps):
+        step()
+        got.append(comm.phase_times())
+    comm.set_phase_timing(False)
+    out = {}
+    for key in ("A", "B", "C", "total"):
+        vals = [g[key] for g in got if g[key] is not None]
+        v = statistics.median(vals) if vals else -1.0
+        t = torch.tensor([v], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        out[key + "_ms"] = None if t.item() < 0 else round(float(t.item()), 4)
+    p = world
+    wire = (p - 1) * nbytes / p          # bytes each rank sends in phase A (and C)
+    if out["A_ms"]:
+        out["A_GBs_per_rank"] = round(wire / (out["A_ms"] * 1e-3) / 1e9, 1)
+    if out["B_ms"]:
+        out["B_hbm_GBs"] = round((p + 1) * nbytes / p / (out["B_ms"] * 1e-3) / 1e9, 1)
+    if out["C_ms"] and coll == "allreduce":
+        out["C_GBs_per_rank"] = round(wire / (out["C_ms"] * 1e-3) / 1e9, 1)
+    out["note"] = ("one untimed step per sample with events between the phases; "
+                   "the pipelined variant overlaps them (total only)")
+    return out
+
+
 def run_multi(args, mvx, dev, world, rank, local):
     import torch
     import torch.distributed as dist
@@ -403,6 +437,7 @@ def run_multi(args, mvx, dev, world, rank, local):
     parity = tried[choice]["parity"]
 
     times = timed(args, step, stream, world)
+    phases = phase_breakdown(comm, step, coll, world, nbytes)
     p = world
     sec = times["t_job"] / args.steps
     if coll == "allreduce":
@@ -416,7 +451,7 @@ def run_multi(args, mvx, dev, world, rank, local):
     roof = {"bound": "xgmi", "achieved": round(busbw, 1), "peak": peak, "unit": "GB/s",
             "frac": round(busbw / peak, 4), "traffic": None, "kernel": mvx.last_kernel(),
             "note": "%s against %d direct xGMI links x %.0f GB/s" % (note, links, XGMI_LINK_GBS),
-            "combine_hbm_bytes_per_step": (p + 1) * nbytes // p}
+            "combine_hbm_bytes_per_step": (p + 1) * nbytes // p, "phases": phases}
     out = result(args, world, nbytes, times, {"c3": "f32", "c4": "int64", "c5": "f32+int32"}[cfg],
                  {"workload": "%s: %s %d MiB per rank, RCCL xGMI exchange + reference-order combine"
                               % (cfg, desc, nbytes // MIB),

@@ -84,6 +84,13 @@ int mvx_comm_reserve(MPI_Comm comm, size_t bytes);
 #define MVX_EXCH_COLL 2
 int mvx_comm_set_exchange(MPI_Comm comm, int mode, int slices);
 int mvx_comm_get_exchange(MPI_Comm comm, int *mode, int *slices);
+/* Per-phase timing (diagnostics): with timing on, each device-buffer call
+ * records HIP events on its stream around phase A (exchange), B (combine)
+ * and C (distribution).  mvx_comm_phase_times waits for the last timed call
+ * and returns ms[0..2] = A, B, C (-1 for the pipelined variant, whose phases
+ * overlap) and ms[3] = the whole call; MPI_ERR_OTHER if nothing was timed. */
+int mvx_comm_set_phase_timing(MPI_Comm comm, int on);
+int mvx_comm_phase_times(MPI_Comm comm, float *ms);
 
 /* ---- MPI API (blocking) ------------------------------------------------ */
 int MPI_Reduce(void *sendbuf, void *recvbuf, int count, MPI_Datatype datatype,

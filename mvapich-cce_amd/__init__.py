@@ -140,6 +140,8 @@ def _load():
     c.mvx_comm_reserve.argtypes = [i, sz]
     c.mvx_comm_set_exchange.argtypes = [i, i, i]
     c.mvx_comm_get_exchange.argtypes = [i, pi, pi]
+    c.mvx_comm_set_phase_timing.argtypes = [i, i]
+    c.mvx_comm_phase_times.argtypes = [i, ctypes.POINTER(ctypes.c_float)]
     c.MPI_Comm_size.argtypes = [i, pi]
     c.MPI_Comm_rank.argtypes = [i, pi]
     c.mvx_buffer_is_device.argtypes = [vp]

@@ -174,6 +174,21 @@ class Comm:
             raise RuntimeError("mvx_comm_get_exchange rc=%d" % rc)
         return m.value, s.value
 
+    def set_phase_timing(self, on=True):
+        """Record HIP events around phases A / B / C of every device call
+        (mvx_comm_set_phase_timing)."""
+        return coll().mvx_comm_set_phase_timing(self.handle, 1 if on else 0)
+
+    def phase_times(self):
+        """{'A', 'B', 'C', 'total'} in ms of the last timed device call
+        (None for a phase of the pipelined variant, whose phases overlap)."""
+        ms = (ctypes.c_float * 4)()
+        rc = coll().mvx_comm_phase_times(self.handle, ms)
+        if rc:
+            raise RuntimeError("mvx_comm_phase_times rc=%d" % rc)
+        v = [None if x < 0 else round(float(x), 5) for x in ms]
+        return {"A": v[0], "B": v[1], "C": v[2], "total": v[3]}
+
     def get_tuning(self):
         """The communicator's device flavour and knobs (a Tuning)."""
         from . import Tuning

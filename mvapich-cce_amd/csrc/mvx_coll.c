@@ -77,6 +77,9 @@ typedef struct {
     mvx_transport ops;
     hipStream_t cstream;        /* combine stream of the pipelined exchange */
     hipEvent_t pev[4];          /* its exchange-done / combine-done events */
+    int timing;                 /* mvx_comm_set_phase_timing: events around phases A / B / C */
+    int tev_ready, tev_kind;    /* events created; what the last timed call recorded (TEV_*) */
+    hipEvent_t tev[4];          /* start, after A, after B, after C */
 } mvx_comm_t;
 
 static mvx_comm_t g_comms[MAX_COMMS];
@@ -292,6 +295,10 @@ int mvx_comm_free(MPI_Comm *comm)
         hipStreamDestroy(c->cstream);
         for (i = 0; i < 4; i++) hipEventDestroy(c->pev[i]);
     }
+    if (c->tev_ready) {
+        int i;
+        for (i = 0; i < 4; i++) hipEventDestroy(c->tev[i]);
+    }
     release_shmem_block(c);
     if (c->handle == MPI_COMM_WORLD) g_have_world = 0;
     memset(c, 0, sizeof *c);
@@ -352,6 +359,53 @@ int mvx_comm_get_exchange(MPI_Comm comm, int *mode, int *slices)
     if (mode) *mode = c->exch;
     if (slices) *slices = c->exch_slices;
     return MPI_SUCCESS;
+}
+
+/* ---- per-phase timing of device calls -----------------------------------
+ * With timing on, every device-buffer call records four events on its
+ * stream: before phase A, after A, after B, after C (the pipelined variant,
+ * whose phases overlap, records only the first and the last). */
+#define TEV_NONE 0
+#define TEV_PHASES 1
+#define TEV_TOTAL 2
+
+int mvx_comm_set_phase_timing(MPI_Comm comm, int on)
+{
+    mvx_comm_t *c = get_comm(comm);
+    int i;
+    if (!c) return ERR_COMM_NULL_CODE;
+    if (on && !c->tev_ready) {
+        if (hipSetDevice(c->device) != hipSuccess) return MPI_ERR_OTHER;
+        for (i = 0; i < 4; i++)
+            if (hipEventCreate(&c->tev[i]) != hipSuccess) return MPI_ERR_OTHER;
+        c->tev_ready = 1;
+    }
+    c->timing = on ? 1 : 0;
+    c->tev_kind = TEV_NONE;
+    return MPI_SUCCESS;
+}
+
+int mvx_comm_phase_times(MPI_Comm comm, float *ms)
+{
+    mvx_comm_t *c = get_comm(comm);
+    int i;
+    if (!c) return ERR_COMM_NULL_CODE;
+    if (!ms) return MPI_ERR_ARG;
+    if (c->tev_kind == TEV_NONE) return MPI_ERR_OTHER;
+    if (hipEventSynchronize(c->tev[3]) != hipSuccess) return MPI_ERR_OTHER;
+    for (i = 0; i < 3; i++) {
+        ms[i] = -1.0f;
+        if (c->tev_kind == TEV_PHASES && hipEventElapsedTime(&ms[i], c->tev[i], c->tev[i + 1]) != hipSuccess)
+            return MPI_ERR_OTHER;
+    }
+    return hipEventElapsedTime(&ms[3], c->tev[0], c->tev[3]) == hipSuccess ? MPI_SUCCESS : MPI_ERR_OTHER;
+}
+
+/* event i of a timed call (no-op when timing is off) */
+static int tev(mvx_comm_t *c, int i, hipStream_t st)
+{
+    if (!c->timing) return MPI_SUCCESS;
+    return hipEventRecord(c->tev[i], st) == hipSuccess ? MPI_SUCCESS : MPI_ERR_OTHER;
 }
 
 int mvx_comm_set_stream(MPI_Comm comm, void *stream)
@@ -1088,17 +1142,22 @@ static int exec_phase_c(rank_exec_t *X, mvx_xport *t, hipStream_t st)
 /* every local rank through phases A, B, C: one rank over RCCL, or all ranks
  * of a virtual communicator over the loopback transport (whose transfers
  * are paired once every rank has issued its phase) */
-static int exec_group(rank_exec_t *X, mvx_xport *t, int nr, hipStream_t st)
+static int exec_group(rank_exec_t *X, mvx_xport *t, int nr, hipStream_t st, mvx_comm_t *timed)
 {
     int r, rc;
+    if (timed && (rc = tev(timed, 0, st))) return rc;
     for (r = 0; r < nr; r++)
         if ((rc = exec_phase_a(&X[r], &t[r], st))) return rc;
     if (t[0].lb && (rc = lb_flush(t[0].lb, st))) return rc;
+    if (timed && (rc = tev(timed, 1, st))) return rc;
     for (r = 0; r < nr; r++)
         if ((rc = exec_phase_b(&X[r], st))) return rc;
+    if (timed && (rc = tev(timed, 2, st))) return rc;
     for (r = 0; r < nr; r++)
         if ((rc = exec_phase_c(&X[r], &t[r], st))) return rc;
     if (t[0].lb && (rc = lb_flush(t[0].lb, st))) return rc;
+    if (timed && (rc = tev(timed, 3, st))) return rc;
+    if (timed && timed->timing) timed->tev_kind = TEV_PHASES;
     return MPI_SUCCESS;
 }
 
@@ -1259,7 +1318,7 @@ static int run_device_plain(mvx_comm_t *c, const job_t *J, hipStream_t st)
         X[r].recvbuf = J->recv[r];
     }
     if ((rc = job_layout(c, X, J, J->P))) return rc;
-    return exec_group(X, J->t, J->nr, st);
+    return exec_group(X, J->t, J->nr, st, c);
 }
 
 static int run_device_pipe(mvx_comm_t *c, const job_t *J, hipStream_t st)
@@ -1283,6 +1342,7 @@ static int run_device_pipe(mvx_comm_t *c, const job_t *J, hipStream_t st)
     }
     region = region_layout(c, X0, J, g_pipe[0], off);   /* slice 0 is the largest */
     if ((rc = grow(&c->pool, &c->pool_bytes, 2 * region))) return rc;
+    if ((rc = tev(c, 0, st))) return rc;
     for (t = 0; t < nsl + 2; t++) {
         const int a = t < nsl, dist = t >= 2;
         const int cur = (int)(t % 3), old = (int)((t + 1) % 3);   /* old = (t - 2) % 3 */
@@ -1312,6 +1372,8 @@ static int run_device_pipe(mvx_comm_t *c, const job_t *J, hipStream_t st)
             if ((rc = exec_phase_b(&X[cur][q], c->cstream))) return rc;
         if (hipEventRecord(c->pev[2 + (int)(t & 1)], c->cstream) != hipSuccess) return MPI_ERR_OTHER;
     }
+    if ((rc = tev(c, 3, st))) return rc;
+    if (c->timing) c->tev_kind = TEV_TOTAL;
     return MPI_SUCCESS;
 }
 
@@ -1357,14 +1419,19 @@ static int run_device_coll(mvx_comm_t *c, const job_t *J, long b, hipStream_t st
     X.wide_n = wide_temps(P);
     X.wide_slot = al256(bb + SLOT_STAGGER);
     if ((rc = grow(&c->pool, &c->pool_bytes, stage + X.wide_slot * (size_t)X.wide_n))) return rc;
+    if ((rc = tev(c, 0, st))) return rc;
     if (ncclAllToAll(J->send[0], c->pool, bb, ncclUint8, c->nccl, st) != ncclSuccess) return MPI_ERR_OTHER;
+    if ((rc = tev(c, 1, st))) return rc;
     for (s = 0; s < P->p; s++)
         leafp[s] = s == P->rank ? J->send[0] + (size_t)P->rank * bb : c->pool + (size_t)s * bb;
     S.base = c->pool + stage; S.slot = X.wide_slot; S.used = 0; S.cap = X.wide_n;
     if ((rc = combine(c, P, leafp, J->recv[0] + P->c_dst_off * P->esize, &S, st))) return rc;
+    if ((rc = tev(c, 2, st))) return rc;
     if (P->coll == MVX_COLL_ALLREDUCE &&
         ncclAllGather(J->recv[0] + (size_t)P->rank * bb, J->recv[0], bb, ncclUint8, c->nccl, st) != ncclSuccess)
         return MPI_ERR_OTHER;
+    if ((rc = tev(c, 3, st))) return rc;
+    if (c->timing) c->tev_kind = TEV_PHASES;
     return MPI_SUCCESS;
 }
 
@@ -1580,7 +1647,7 @@ static int run_staged(mvx_comm_t *c, const job_t *J, hipStream_t st)
             X[r].P = &Q[r];
         }
         if ((rc = stage_in(&S, Q, i, st))) return rc;
-        if ((rc = exec_group(X, J->t, J->nr, st))) return rc;
+        if ((rc = exec_group(X, J->t, J->nr, st, NULL))) return rc;
         if ((rc = stage_out(&S, Q, i, st))) return rc;
         if (i > 0 && (rc = stage_drain(&S, g_slice[(i - 1) & 1], i - 1, st))) return rc;
     }

@@ -94,6 +94,10 @@ def test_null_communicator_codes(mvx):
     assert mvx.MPI_Allreduce(0, 0, 1, 10, 102, 12345) == 5 | (3 << 6)
     assert mvx.MPI_Reduce(0, 0, 1, 10, 102, 0, 12345) == 5 | (3 << 6)
     assert mvx.MPI_Reduce_scatter(0, 0, [1], 10, 102, 12345) == 5 | (3 << 6)
+    import ctypes
+    c = mvx.coll()
+    assert c.mvx_comm_set_phase_timing(12345, 1) == 5 | (3 << 6)
+    assert c.mvx_comm_phase_times(12345, (ctypes.c_float * 4)()) == 5 | (3 << 6)
 
 
 def test_plan_rejects_bad_arguments(mvx):

@@ -225,3 +225,39 @@ def test_pipelined_exchange_matches_reference(mvx, oracle, slices, p):
                     T.assert_same(op, dtype, T.from_dev(drs[q])[: cnt * E], R0[q][:cnt], typemap_only=True)
     finally:
         comm.free()
+
+
+@pytest.mark.parametrize("mode", ["p2p", "pipe"])
+def test_phase_timing(mvx, mode):
+    """mvx_comm_set_phase_timing: events around phases A / B / C of a device
+    call; the pipelined variant (overlapping phases) reports the total only.
+    Timing does not change the result."""
+    import torch
+    p, n = 4, 1 << 22
+    comm = mvx.Comm.local_ranks(p, 0)
+    try:
+        if mode == "pipe":
+            assert comm.set_exchange(mvx.EXCH_PIPE, 4) == 0
+        with pytest.raises(RuntimeError):
+            comm.phase_times()               # nothing timed yet
+        S = [T.rand_vec(10, n, 77 + r) for r in range(p)]
+        ds = [T.to_dev(s) for s in S]
+        outs = []
+        for timed in (False, True):
+            assert comm.set_phase_timing(timed) == 0
+            dr = [torch.zeros(n * 4, dtype=torch.uint8, device="cuda") for _ in range(p)]
+            r, rcs = comm.allreduce_multi(ds, dr, n, 10, 102)
+            assert r == 0 and rcs == [0] * p
+            outs.append([T.from_dev(x) for x in dr])
+        ph = comm.phase_times()
+        assert ph["total"] > 0
+        if mode == "p2p":
+            assert ph["A"] > 0 and ph["B"] > 0 and ph["C"] > 0
+            assert ph["A"] + ph["B"] + ph["C"] <= ph["total"] * 1.01 + 1e-3
+        else:
+            assert ph["A"] is None and ph["B"] is None and ph["C"] is None
+        for a, b in zip(*outs):
+            assert np.array_equal(a, b)
+        assert comm.set_phase_timing(False) == 0
+    finally:
+        comm.free()

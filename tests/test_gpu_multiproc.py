@@ -101,3 +101,5 @@ def test_bench_multi_gpu_leg_host_transport(cfg):
     assert all(v["parity"] for v in d["config"]["exchange_tuning"].values()), d["config"]["exchange_tuning"]
     assert d["cpu_baseline"]["cores"] == 2
     assert d["config"]["transport"] == "host"
+    ph = d["roofline"]["phases"]
+    assert ph["total_ms"] > 0, ph
