@@ -68,10 +68,11 @@ static struct {
 } g_pc = { PTHREAD_MUTEX_INITIALIZER, PTHREAD_COND_INITIALIZER, PTHREAD_COND_INITIALIZER,
            -1, 0, 0, NULL, NULL, 0 };
 
-/* part `i` of `n` of a copy, split at 4 KiB */
+/* part `i` of `n` of a copy, split at 4 KiB (parts are ceil(bytes / n)
+ * rounded up, so the n parts cover every byte) */
 static void pc_part(int i, int n, char *dst, const char *src, size_t bytes)
 {
-    const size_t per = ((bytes / (size_t)n) + 4095) & ~(size_t)4095;
+    const size_t per = ((bytes + (size_t)n - 1) / (size_t)n + 4095) & ~(size_t)4095;
     const size_t lo = per * (size_t)i;
     size_t hi = lo + per;
     if (lo >= bytes) return;

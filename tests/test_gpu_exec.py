@@ -261,3 +261,29 @@ def test_phase_timing(mvx, mode):
         assert comm.set_phase_timing(False) == 0
     finally:
         comm.free()
+
+
+@pytest.mark.parametrize("n", [262145, 2097153, 786433])
+@pytest.mark.parametrize("p", [1, 2])
+@pytest.mark.parametrize("coll", ["ar", "red", "rs", "scan"])
+def test_pageable_ragged_sizes(mvx, oracle, n, p, coll):
+    """Pageable host buffers whose byte size divided by the copy pool's
+    threads falls on a 4 KiB boundary with a remainder (1 MiB + 4 B,
+    8 MiB + 4 B, 3 MiB + 4 B of floats): the bounce copies carry every byte
+    (a split that rounded down dropped the last bytes % threads bytes)."""
+    comm = mvx.Comm.local_ranks(p, 0)
+    try:
+        dtype, op, E = 10, 102, 4
+        cnts = [n] * p if coll == "rs" else None
+        tot = n * p if cnts else n
+        S = [T.rand_vec(dtype, tot, 31 * n + r) for r in range(p)]
+        sends = [T.clone(s).view(np.uint8) for s in S]
+        recvs = [np.zeros(n * E, np.uint8) for _ in range(p)]
+        r, rcs = _call(comm, coll, sends, recvs, cnts if cnts else n, dtype, op, 0)
+        assert r == 0
+        R0 = [np.zeros(n, S[0].dtype) for _ in range(p)]
+        assert rcs == _oracle_coll(oracle, coll, S, R0, cnts if cnts else n, dtype, op, 0)
+        for q in ([0] if coll == "red" else range(p)):
+            T.assert_same(op, dtype, recvs[q], R0[q], typemap_only=True)
+    finally:
+        comm.free()

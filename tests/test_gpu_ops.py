@@ -133,7 +133,7 @@ def _back(y, kind):
     return np.asarray(y)
 
 
-@pytest.mark.parametrize("n", [1, 1000, 9 * 1024 * 1024 + 5, 17 * 1024 * 1024 + 3])
+@pytest.mark.parametrize("n", [1, 1000, 9 * 1024 * 1024 + 5, 17 * 1024 * 1024 + 3, 16 * 1024 * 1024 + 262145])
 @pytest.mark.parametrize("where", ["host-host", "dev-host", "host-dev", "pin-pin", "pin-host", "host-pin",
                                    "dev-pin"])
 def test_mpir_host_buffers(mvx, oracle, n, where):
