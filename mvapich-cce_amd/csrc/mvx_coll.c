@@ -80,6 +80,7 @@ typedef struct {
     int timing;                 /* mvx_comm_set_phase_timing: events around phases A / B / C */
     int tev_ready, tev_kind;    /* events created; what the last timed call recorded (TEV_*) */
     hipEvent_t tev[4];          /* start, after A, after B, after C */
+    int keep;                   /* this call's (op, type) is undefined: every combine keeps its inout */
 } mvx_comm_t;
 
 static mvx_comm_t g_comms[MAX_COMMS];
@@ -941,6 +942,16 @@ static int combine(mvx_comm_t *c, const mvx_plan *P, const char *const *leafp, v
     for (q = 0; q < P->k; q++) {
         srcs[q] = leafp[P->leaf[q]];
         fold[q] = P->leaf_fold[q] >= 0 ? leafp[P->leaf_fold[q]] : NULL;
+    }
+    if (c->keep) {
+        /* an undefined (op, type): the reference's op functions return with
+         * inoutvec untouched (global_ops.c, e.g. 401-404), and every step's
+         * left operand is the inout one (mvx_plan), so the program's result
+         * is leaf 0 as it arrived -- packed or not, the same bytes */
+        const size_t nb = (size_t)(P->c_cnt * P->esize);
+        if (!nb || srcs[0] == dst) return MPI_SUCCESS;
+        return hipMemcpyAsync(dst, srcs[0], nb, hipMemcpyDeviceToDevice, st) == hipSuccess ? MPI_SUCCESS
+                                                                                        : MPI_ERR_OTHER;
     }
     if (P->packed) return combine_packed(c, P, srcs, fold, dst, st);
     if (P->opkind != MVX_OPKIND_PREDEFINED)
@@ -1817,12 +1828,21 @@ static void call_sizes(const call_t *k, int p, int rank, long *nsend, long *nrec
     }
 }
 
+/* An undefined (op, type) still runs the reference's transfers, with ops
+ * that leave their inout operand as it is -- except under the _SMP_ collops,
+ * whose len = 0 test of a predefined op (intra_fns_new.c:5054-5058,
+ * 5841-5845) returns on every rank before anything moves. */
+static int undefined_moves(const mvx_comm_t *c, int coll)
+{
+    return !(c->tune.smp && (coll == MVX_COLL_ALLREDUCE || coll == MVX_COLL_REDUCE));
+}
+
 static int run(mvx_comm_t *c, const call_t *k, hipStream_t st, int blocking)
 {
     static mvx_plan P;
     job_t J;
     mvx_xport t;
-    int rc, verdict;
+    int rc, verdict, keep = 0, vrc = MPI_SUCCESS;
     long nsend, nrecv;
     int e, ts;
 
@@ -1842,8 +1862,15 @@ static int run(mvx_comm_t *c, const call_t *k, hipStream_t st, int blocking)
             return MPI_ERR_OTHER;
         return (blocking && hipStreamSynchronize(st) != hipSuccess) ? MPI_ERR_OTHER : MPI_SUCCESS;
     }
-    if (verdict == MVX_ERR_OP_NOT_DEFINED) return P.calls_uop ? verdict : MPI_SUCCESS;
-    if (verdict) return verdict;
+    if (verdict == MVX_ERR_OP_NOT_DEFINED) {
+        /* 329 on the ranks that call (*uop); the data still moves as the
+         * reference's algorithm moves it (undefined_moves) */
+        vrc = P.calls_uop ? verdict : MPI_SUCCESS;
+        if (!undefined_moves(c, k->coll)) return vrc;
+        keep = 1;
+    } else if (verdict) {
+        return verdict;
+    }
 
     memset(&t, 0, sizeof t);
     if (c->has_ops) {
@@ -1862,7 +1889,10 @@ static int run(mvx_comm_t *c, const call_t *k, hipStream_t st, int blocking)
     J.nsend[0] = nsend;
     J.nrecv[0] = nrecv;
     J.t = &t;
-    return run_job(c, &J, st, blocking);
+    c->keep = keep;
+    rc = run_job(c, &J, st, blocking);
+    c->keep = 0;
+    return rc ? rc : vrc;
 }
 
 /* ---------------------------------------------------------------------- */
@@ -2089,7 +2119,8 @@ static int run_multi(mvx_comm_t *c, int coll, void *const *sendbufs,
                 }
             }
         }
-        return MPI_SUCCESS;
+        if (verdict != MVX_ERR_OP_NOT_DEFINED || coll == MVX_COLL_SCAN || !undefined_moves(c, coll))
+            return MPI_SUCCESS;
     }
     k.coll = coll; k.count = count; k.recvcnts = recvcnts; k.root = root;
     J.nr = p;
@@ -2107,8 +2138,11 @@ static int run_multi(mvx_comm_t *c, int coll, void *const *sendbufs,
     }
     J.kinds = 0;
     host = job_kinds(&J);
-    if (plans[0].packed) return run_job_packed(c, &J, st, host);
-    return host ? run_staged(c, &J, st) : run_device(c, &J, st);
+    c->keep = verdict == MVX_ERR_OP_NOT_DEFINED;    /* the transfers of an undefined pair */
+    if (plans[0].packed) rc = run_job_packed(c, &J, st, host);
+    else rc = host ? run_staged(c, &J, st) : run_device(c, &J, st);
+    c->keep = 0;
+    return rc;
 }
 
 int mvx_allreduce_multi(void *const *sendbufs, void *const *recvbufs, int count,

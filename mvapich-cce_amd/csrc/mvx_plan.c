@@ -168,6 +168,9 @@ static int is_ieee(int t)
 static int op_symmetric(int op, int dtype)
 {
     int old = dtype, cnt = 1;
+    /* an undefined pair leaves every inout operand as it is (global_ops.c's
+     * default branches): the result is the inout leaf's, so roles matter */
+    if (!mvx_op_supported(op, dtype)) return 0;
     if (dtype == MPI_LONG_DOUBLE || dtype == MPI_LONG_DOUBLE_INT) return 0;
     if (dtype >= MVX_TYPE_DERIVED_BASE || dtype == MPI_2REAL || dtype == MPI_2DOUBLE_PRECISION) {
         /* count-2 contiguous {value, loc} pairs of one base type: the IEEE /

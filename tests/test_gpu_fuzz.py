@@ -1,0 +1,158 @@
+"""Seeded random sweep over the whole device path against the oracle's
+replay of the reference schedules (oracle/coll_sim.c): communicator size,
+collective, (op, datatype) -- undefined pairs included, whose 329 must come
+from exactly the ranks the reference's (*uop) calls would --, count (0,
+ragged, across the algorithm thresholds and the staging-slice sizes), root,
+ragged recvcnts, exchange variant (p2p / pipe with 2-6 slices / coll),
+device flavour (ch_shmem / _SMP_) and buffer kind per rank (HBM, pageable,
+page-locked, mixed, and offset by one element from the allocation).
+
+Each case is one call on a virtual communicator; every rank's result and
+return code must equal the reference's.  MVX_FUZZ_CASES / MVX_FUZZ_SEED
+widen or move the sweep."""
+import os
+
+import numpy as np
+import pytest
+
+import mvxtest as T
+
+pytestmark = pytest.mark.gpu
+
+N_CASES = int(os.environ.get("MVX_FUZZ_CASES", "600"))
+SEED = int(os.environ.get("MVX_FUZZ_SEED", "20261017"))
+BATCH = 40
+TYPES = [t for t in T.ALL_TYPES]
+MAX_BYTES = 24 << 20          # per rank vector
+
+
+def _case(rng, mvx):
+    p = int(rng.choice([1, 2, 2, 3, 4, 4, 5, 6, 7, 8, 8, 9, 12]))
+    coll = str(rng.choice(["ar", "ar", "red", "rs", "scan"]))
+    dtype = int(rng.choice(TYPES))
+    op = int(rng.integers(100, 112))
+    E = mvx.dtype_info(dtype)[0]
+    r = rng.random()
+    if r < 0.08:
+        n = 0
+    elif r < 0.45:
+        n = int(rng.integers(1, 300))
+    elif r < 0.85:
+        n = int(np.exp2(rng.uniform(8, 17)))
+    else:
+        n = int(np.exp2(rng.uniform(17, 21)))
+    n = min(n, MAX_BYTES // E // (p if coll == "rs" else 1))
+    cnts = None
+    if coll == "rs":
+        base = max(n // max(p, 1), 0)
+        cnts = [int(max(0, base + rng.integers(-3, 4))) if rng.random() < 0.8 else 0 for _ in range(p)]
+    exch = str(rng.choice(["p2p", "pipe", "coll"]))
+    slices = int(rng.integers(2, 7))
+    smp = bool(rng.random() < 0.25)
+    kinds = [str(rng.choice(["dev", "dev", "host", "pin"])) for _ in range(2 * p)]
+    shift = [int(rng.random() < 0.2) for _ in range(2 * p)]
+    root = int(rng.integers(0, p))
+    return dict(p=p, coll=coll, dtype=dtype, op=op, n=n, cnts=cnts, exch=exch, slices=slices, smp=smp,
+                kinds=kinds, shift=shift, root=root, seed=int(rng.integers(1 << 30)))
+
+
+def _place(a_u8, kind, shift, E):
+    """A buffer of kind `kind` holding bytes a_u8, `shift` elements into its
+    allocation; returns (buffer, allocation) -- the allocation keeps it alive."""
+    import torch
+    off = shift * E
+    nb = a_u8.nbytes
+    if kind == "host":
+        whole = np.zeros(nb + off + 1, np.uint8)
+        whole[off:off + nb] = a_u8
+        return whole[off:off + max(nb, 1)], whole
+    if kind == "pin":
+        whole = torch.zeros(nb + off + 1, dtype=torch.uint8, pin_memory=True)
+        whole.numpy()[off:off + nb] = a_u8
+        return whole[off:off + max(nb, 1)], whole
+    whole = torch.zeros(nb + off + 1, dtype=torch.uint8, device="cuda")
+    if nb:
+        whole[off:off + nb] = torch.from_numpy(np.ascontiguousarray(a_u8)).to("cuda")
+    return whole[off:off + max(nb, 1)], whole
+
+
+def _back(buf):
+    import torch
+    if isinstance(buf, torch.Tensor):
+        if buf.is_cuda:
+            torch.cuda.synchronize()
+        return buf.cpu().numpy()
+    return buf
+
+
+@pytest.fixture(scope="module")
+def comms(mvx):
+    cs = {}
+    yield cs
+    for c in cs.values():
+        c.free()
+
+
+def _run_case(mvx, oracle, comms, c):
+    p, coll, dtype, op, n = c["p"], c["coll"], c["dtype"], c["op"], c["n"]
+    E = mvx.dtype_info(dtype)[0]
+    if p not in comms:
+        comms[p] = mvx.Comm.local_ranks(p, 0)
+    comm = comms[p]
+    mode = {"p2p": mvx.EXCH_P2P, "pipe": mvx.EXCH_PIPE, "coll": mvx.EXCH_COLL}[c["exch"]]
+    assert comm.set_exchange(mode, c["slices"]) == 0
+    assert comm.set_tuning(mvx.smp_tuning() if c["smp"] else mvx.tuning_from_env(smp=False)) == 0
+    cnts = c["cnts"]
+    tot = sum(cnts) if cnts else n
+    S = [T.rand_vec(dtype, tot, c["seed"] + q) for q in range(p)]
+    rcount = [(cnts[q] if cnts else n) for q in range(p)]
+    keep, sends, recvs = [], [], []
+    for q in range(p):
+        b, w = _place(np.ascontiguousarray(S[q]).view(np.uint8), c["kinds"][2 * q], c["shift"][2 * q], E)
+        sends.append(b)
+        keep.append(w)
+        b, w = _place(np.zeros(rcount[q] * E, np.uint8), c["kinds"][2 * q + 1], c["shift"][2 * q + 1], E)
+        recvs.append(b)
+        keep.append(w)
+    if coll == "ar":
+        r, rcs = comm.allreduce_multi(sends, recvs, n, dtype, op)
+    elif coll == "red":
+        r, rcs = comm.reduce_multi(sends, recvs, n, dtype, op, c["root"])
+    elif coll == "scan":
+        r, rcs = comm.scan_multi(sends, recvs, n, dtype, op)
+    else:
+        r, rcs = comm.reduce_scatter_multi(sends, recvs, cnts, dtype, op)
+    assert r == 0, (r, c)
+    R0 = [np.zeros(max(rcount[q], 1), S[0].dtype) for q in range(p)]
+    s8 = [s.view(np.uint8) for s in S]
+    r8 = [x.view(np.uint8) for x in R0]
+    oracle.smp_set(1 if c["smp"] else 0)
+    try:
+        if coll == "ar":
+            rref = oracle.allreduce(s8, r8, n, dtype, op)
+        elif coll == "red":
+            rref = oracle.reduce(s8, r8, n, dtype, op, c["root"])
+        elif coll == "scan":
+            rref = oracle.scan(s8, r8, n, dtype, op)
+        else:
+            rref = oracle.reduce_scatter(s8, r8, cnts, dtype, op)
+    finally:
+        oracle.smp_set(0)
+    assert list(rcs) == list(rref), (rcs, rref, c)
+    for q in range(p):
+        if coll == "red" and q != c["root"]:
+            continue
+        if rcs[q]:
+            continue                      # an undefined pair: the reference leaves recvbuf unspecified
+        got = _back(recvs[q])
+        try:
+            T.assert_same(op, dtype, got[: rcount[q] * E], R0[q][: rcount[q]], typemap_only=True)
+        except AssertionError as e:
+            raise AssertionError("rank %d of %s: %s" % (q, c, e))
+
+
+@pytest.mark.parametrize("batch", range((N_CASES + BATCH - 1) // BATCH))
+def test_random_sweep(mvx, oracle, comms, batch):
+    rng = np.random.default_rng(SEED + batch)
+    for _ in range(min(BATCH, N_CASES - batch * BATCH)):
+        _run_case(mvx, oracle, comms, _case(rng, mvx))
