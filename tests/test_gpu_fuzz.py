@@ -4,8 +4,10 @@ collective, (op, datatype) -- undefined pairs included, whose 329 must come
 from exactly the ranks the reference's (*uop) calls would --, count (0,
 ragged, across the algorithm thresholds and the staging-slice sizes), root,
 ragged recvcnts, exchange variant (p2p / pipe with 2-6 slices / coll),
-device flavour (ch_shmem / _SMP_) and buffer kind per rank (HBM, pageable,
-page-locked, mixed, and offset by one element from the allocation).
+device flavour (ch_shmem / _SMP_), buffer kind per rank (HBM, pageable,
+page-locked, mixed, and offset by one element from the allocation), and
+user-defined ops (host MPI_User_functions and device functions, commutative
+or not, tests/user_ops.c / user_ops_dev.hip).
 
 Each case is one call on a virtual communicator; every rank's result and
 return code must equal the reference's.  MVX_FUZZ_CASES / MVX_FUZZ_SEED
@@ -16,6 +18,7 @@ import numpy as np
 import pytest
 
 import mvxtest as T
+import uops
 
 pytestmark = pytest.mark.gpu
 
@@ -24,6 +27,7 @@ SEED = int(os.environ.get("MVX_FUZZ_SEED", "20261017"))
 BATCH = 40
 TYPES = [t for t in T.ALL_TYPES]
 MAX_BYTES = 24 << 20          # per rank vector
+DEVICE_UOPS = ["addem", "affine", "fsum", "mix"]   # the ops tests/user_ops_dev.hip also defines
 
 
 def _case(rng, mvx):
@@ -52,8 +56,16 @@ def _case(rng, mvx):
     kinds = [str(rng.choice(["dev", "dev", "host", "pin"])) for _ in range(2 * p)]
     shift = [int(rng.random() < 0.2) for _ in range(2 * p)]
     root = int(rng.integers(0, p))
+    uop = None
+    if rng.random() < 0.2:
+        device = bool(rng.random() < 0.5)
+        names = DEVICE_UOPS if device else sorted(uops.UOPS)
+        uop = (str(rng.choice(names)), int(rng.integers(0, 2)), device)
+        n = min(n, 1 << 18)
+        if cnts:
+            cnts = [min(x, (1 << 18) // p) for x in cnts]
     return dict(p=p, coll=coll, dtype=dtype, op=op, n=n, cnts=cnts, exch=exch, slices=slices, smp=smp,
-                kinds=kinds, shift=shift, root=root, seed=int(rng.integers(1 << 30)))
+                kinds=kinds, shift=shift, root=root, seed=int(rng.integers(1 << 30)), uop=uop)
 
 
 def _place(a_u8, kind, shift, E):
@@ -89,12 +101,38 @@ def _back(buf):
 def comms(mvx):
     cs = {}
     yield cs
-    for c in cs.values():
-        c.free()
+    for key, c in cs.items():
+        if key == "ops":
+            for h in c.values():
+                mvx.MPI_Op_free(h)
+        else:
+            c.free()
+
+
+def _user_op(mvx, comms, name, commute, device):
+    """Product handle of a user op (created once per module); the oracle
+    runs the same host function under handle 250."""
+    ops = comms.setdefault("ops", {})
+    key = (name, commute, device)
+    if key not in ops:
+        if device:
+            rc, h = mvx.op_create_device(uops.dev_fn(name), commute)
+        else:
+            rc, h = mvx.MPI_Op_create(uops.host_fn(name), commute)
+        assert rc == 0
+        ops[key] = h
+    return ops[key]
 
 
 def _run_case(mvx, oracle, comms, c):
     p, coll, dtype, op, n = c["p"], c["coll"], c["dtype"], c["op"], c["n"]
+    oracle_op = op
+    if c["uop"]:
+        name, commute, device = c["uop"]
+        dtype = uops.UOPS[name][0]
+        op = _user_op(mvx, comms, name, commute, device)
+        oracle_op = 250
+        assert oracle.user_op_set(250, uops.host_fn(name), commute) == 0
     E = mvx.dtype_info(dtype)[0]
     if p not in comms:
         comms[p] = mvx.Comm.local_ranks(p, 0)
@@ -104,7 +142,10 @@ def _run_case(mvx, oracle, comms, c):
     assert comm.set_tuning(mvx.smp_tuning() if c["smp"] else mvx.tuning_from_env(smp=False)) == 0
     cnts = c["cnts"]
     tot = sum(cnts) if cnts else n
-    S = [T.rand_vec(dtype, tot, c["seed"] + q) for q in range(p)]
+    if c["uop"]:
+        S = [uops.rand_for(c["uop"][0], tot, c["seed"] + q) for q in range(p)]
+    else:
+        S = [T.rand_vec(dtype, tot, c["seed"] + q) for q in range(p)]
     rcount = [(cnts[q] if cnts else n) for q in range(p)]
     keep, sends, recvs = [], [], []
     for q in range(p):
@@ -129,13 +170,13 @@ def _run_case(mvx, oracle, comms, c):
     oracle.smp_set(1 if c["smp"] else 0)
     try:
         if coll == "ar":
-            rref = oracle.allreduce(s8, r8, n, dtype, op)
+            rref = oracle.allreduce(s8, r8, n, dtype, oracle_op)
         elif coll == "red":
-            rref = oracle.reduce(s8, r8, n, dtype, op, c["root"])
+            rref = oracle.reduce(s8, r8, n, dtype, oracle_op, c["root"])
         elif coll == "scan":
-            rref = oracle.scan(s8, r8, n, dtype, op)
+            rref = oracle.scan(s8, r8, n, dtype, oracle_op)
         else:
-            rref = oracle.reduce_scatter(s8, r8, cnts, dtype, op)
+            rref = oracle.reduce_scatter(s8, r8, cnts, dtype, oracle_op)
     finally:
         oracle.smp_set(0)
     assert list(rcs) == list(rref), (rcs, rref, c)
@@ -149,7 +190,8 @@ def _run_case(mvx, oracle, comms, c):
         # every rank, 329 or not: an undefined pair moves the data as the
         # reference's algorithm does (ops that keep their inout operand)
         try:
-            T.assert_same(op, dtype, got[: rcount[q] * E], R0[q][: rcount[q]], typemap_only=True)
+            T.assert_same(0 if c["uop"] else op, dtype, got[: rcount[q] * E], R0[q][: rcount[q]],
+                          typemap_only=True)
         except AssertionError as e:
             raise AssertionError("rank %d of %s: %s" % (q, c, e))
 
