@@ -71,11 +71,23 @@ def test_executor_across_processes_host_transport(world):
         assert not rep["transport_errors"], rep["transport_errors"][:3]
 
 
+@pytest.mark.parametrize("world", [2, 3])
+def test_executor_random_host_transport(world):
+    """A seeded random sweep (collective, op x datatype with the undefined
+    pairs, count, root, exchange variant, device or host buffers) through the
+    one-rank-per-process path; every rank's code and recvbuf against the
+    oracle."""
+    reports = _launch(world, "host", "random", 240)
+    for rep in reports:
+        assert rep["checked"] >= 100
+        assert not rep["fails"], rep["fails"][:5]
+
+
 @pytest.mark.parametrize("world", [2, 4, 8])
 def test_rccl_multirank(world):
     if _ngpus() < world:
         pytest.skip("needs %d GPUs (RCCL refuses two ranks on one GPU)" % world)
-    for suite in ("small", "full"):
+    for suite in ("small", "random", "full"):
         for rep in _launch(world, "rccl", suite, 900):
             assert rep["checked"] > 0
             assert not rep["fails"], rep["fails"][:5]
