@@ -201,3 +201,53 @@ def test_random_sweep(mvx, oracle, comms, batch):
     rng = np.random.default_rng(SEED + batch)
     for _ in range(min(BATCH, N_CASES - batch * BATCH)):
         _run_case(mvx, oracle, comms, _case(rng, mvx))
+
+
+MPIR_NAMES = {100: "MPIR_MAXF", 101: "MPIR_MINF", 102: "MPIR_SUM", 103: "MPIR_PROD", 104: "MPIR_LAND",
+              105: "MPIR_BAND", 106: "MPIR_LOR", 107: "MPIR_BOR", 108: "MPIR_LXOR", 109: "MPIR_BXOR",
+              110: "MPIR_MINLOC", 111: "MPIR_MAXLOC"}
+
+
+def _op_case(rng):
+    dtype = int(rng.choice(TYPES))
+    op = int(rng.integers(100, 112))
+    r = rng.random()
+    if r < 0.5:
+        n = int(rng.integers(0, 5000))
+    elif r < 0.9:
+        n = int(np.exp2(rng.uniform(12, 22)))
+    else:
+        n = int(np.exp2(rng.uniform(22, 24.5)))       # past the 64 MiB bounce threshold
+    return dict(dtype=dtype, op=op, n=n, kin=str(rng.choice(["dev", "host", "pin"])),
+                kio=str(rng.choice(["dev", "host", "pin"])), sin=int(rng.random() < 0.3),
+                sio=int(rng.random() < 0.3), seed=int(rng.integers(1 << 30)))
+
+
+@pytest.mark.parametrize("batch", range(4))
+def test_random_op_functions(mvx, oracle, batch):
+    """The predefined ops through their MPI_User_function symbols (MPIR_SUM
+    ...) on random sizes (up to ~90 MiB), operand kinds (HBM, pageable,
+    page-locked, independently per operand, offset by one element) and
+    (op, datatype) pairs -- undefined ones included, which must set the op
+    errno to 329 and leave inoutvec untouched -- against the oracle's op."""
+    rng = np.random.default_rng(SEED + 1000 + batch)
+    for _ in range(25):
+        c = _op_case(rng)
+        dtype, op, n = c["dtype"], c["op"], c["n"]
+        E = mvx.dtype_info(dtype)[0]
+        n = min(n, (96 << 20) // E)
+        a, b = T.rand_vec(dtype, n, c["seed"]), T.rand_vec(dtype, n, c["seed"] + 1)
+        ia, wa = _place(np.ascontiguousarray(a).view(np.uint8), c["kin"], c["sin"], E)
+        io, wio = _place(np.ascontiguousarray(b).view(np.uint8), c["kio"], c["sio"], E)
+        ref = T.clone(b)
+        rc_ref = oracle.op(op, dtype, np.ascontiguousarray(a).view(np.uint8), ref.view(np.uint8), n)
+        mvx.op_errno()
+        mvx.MPIR_call(MPIR_NAMES[op], ia, io, n, dtype)
+        rc = mvx.op_errno()
+        assert rc == rc_ref, (rc, rc_ref, c)
+        got = _back(io)[: n * E]
+        if n:
+            try:
+                T.assert_same(op, dtype, got, ref)
+            except AssertionError as e:
+                raise AssertionError("%s: %s" % (c, e))
