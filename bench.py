@@ -418,7 +418,11 @@ def run_multi(args, mvx, dev, world, rank, local):
     for name in names:
         mode, slices = EXCH[name]
         comm.set_exchange(mode, slices)
-        ok = check() if ref is not None else None
+        if ref is not None:
+            ok = check()
+        else:
+            ok = None
+            step()      # untimed: RCCL sets up a variant's connections on its first use
         t = torch.zeros(1, dtype=torch.float64)
         torch.cuda.synchronize()
         dist.barrier()
