@@ -250,8 +250,9 @@ def timed(args, step, stream, world):
     for i in range(args.steps):
         step()
     e1.record(stream)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0      # this rank's K steps; MAX over ranks below
     barrier()
-    wall = time.perf_counter() - t0
     dev_ms = e0.elapsed_time(e1)
     evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     evs[0].record(stream)
