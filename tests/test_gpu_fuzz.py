@@ -26,7 +26,8 @@ N_CASES = int(os.environ.get("MVX_FUZZ_CASES", "600"))
 SEED = int(os.environ.get("MVX_FUZZ_SEED", "20261017"))
 BATCH = 40
 TYPES = [t for t in T.ALL_TYPES]
-MAX_BYTES = 24 << 20          # per rank vector
+MAX_BYTES = int(os.environ.get("MVX_FUZZ_MAX_MIB", "24")) << 20     # per rank vector
+BIG = os.environ.get("MVX_FUZZ_BIG") == "1"     # sizes 1 Mi - 64 Mi elements (one-off sweeps)
 DEVICE_UOPS = ["addem", "affine", "fsum", "mix"]   # the ops tests/user_ops_dev.hip also defines
 
 
@@ -37,7 +38,9 @@ def _case(rng, mvx):
     op = int(rng.integers(100, 112))
     E = mvx.dtype_info(dtype)[0]
     r = rng.random()
-    if r < 0.08:
+    if BIG:
+        n = int(np.exp2(rng.uniform(20, 26)))
+    elif r < 0.08:
         n = 0
     elif r < 0.45:
         n = int(rng.integers(1, 300))
