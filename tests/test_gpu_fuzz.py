@@ -32,7 +32,7 @@ DEVICE_UOPS = ["addem", "affine", "fsum", "mix"]   # the ops tests/user_ops_dev.
 
 
 def _case(rng, mvx):
-    p = int(rng.choice([1, 2, 2, 3, 4, 4, 5, 6, 7, 8, 8, 9, 12]))
+    p = int(rng.choice([1, 2, 2, 3, 4, 4, 5, 6, 7, 8, 8, 9, 12, 16, 33]))
     coll = str(rng.choice(["ar", "ar", "red", "rs", "scan"]))
     dtype = int(rng.choice(TYPES))
     op = int(rng.integers(100, 112))
