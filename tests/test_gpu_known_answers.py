@@ -226,3 +226,33 @@ def test_successive_calls_do_not_interfere(mvx, comms, flavour, where, p):
     for x in r:
         got = float(x.cpu()[0]) if where == "device" else float(x[0])
         assert got == 10.0 * p
+
+
+@pytest.mark.parametrize("flavour", ["ch_shmem", "smp"])
+@pytest.mark.parametrize("where", ["device", "host"])
+@pytest.mark.parametrize("p", [2, 4])
+def test_coll8_coll13_known_answers(mvx, comms, flavour, where, p):
+    """examples/test/coll/coll8.c: MPI_Reduce of data = rank to root 0 with
+    MPI_SUM (sum of ranks), MPI_MIN (0) and MPI_MAX (size - 1); coll13.c:
+    MPI_Allreduce(MPI_SUM) of every rank's MPI_Alltoall status (0 -> 0)."""
+    import torch
+    comm = comms[p][flavour]
+
+    def bufs(vals):
+        if where == "device":
+            return ([torch.tensor([v], dtype=torch.int32, device="cuda") for v in vals],
+                    [torch.full((1,), -100, dtype=torch.int32, device="cuda") for _ in vals])
+        return [np.array([v], np.int32) for v in vals], [np.full(1, -100, np.int32) for _ in vals]
+
+    def val(x):
+        return int(x.cpu()[0]) if where == "device" else int(x[0])
+
+    for op, want in ((mvx.MPI_SUM, sum(range(p))), (mvx.MPI_MIN, 0), (mvx.MPI_MAX, p - 1)):
+        s, r = bufs(list(range(p)))
+        rc, rcs = comm.reduce_multi(s, r, 1, mvx.MPI_INT, op, 0)
+        assert rc == 0 and rcs == [0] * p
+        assert val(r[0]) == want, (op, val(r[0]))
+        assert all(val(x) == -100 for x in r[1:])         # non-roots: recvbuf untouched
+    s, r = bufs([0] * p)
+    rc, rcs = comm.allreduce_multi(s, r, 1, mvx.MPI_INT, mvx.MPI_SUM)
+    assert rc == 0 and all(val(x) == 0 for x in r)
