@@ -674,8 +674,16 @@ static KSet kset(const char *name)
     // the standalone sweep, profiles/r02/tune_occ_k2.jsonl, but 124.8 vs
     // 123.5-124.8 us in the product: not adopted)
     s.prog = kfam<O, T, MVX_COMBINE_KMAX, 1, 1, 0>(FAM_PROG);
-    s.tree8 = kfam<O, T, 8, 1, 2, 1>(FAM_TREE);
-    s.tree4 = kfam<O, T, 4, 1, 2, 1>(FAM_TREE);
+    if constexpr (alu_heavy<T>::v) {
+        // x87 (integer-emulated, ALU-bound) trees: U = 1 keeps 53-57 VGPRs
+        // and 7-8 waves per SIMD (U = 2: 98, 4 waves); SUM tree k = 8 57.6 ->
+        // 53.3 us (profiles/r02/bench_kernels_x87.jsonl)
+        s.tree8 = kfam<O, T, 8, 1, 1, 1>(FAM_TREE);
+        s.tree4 = kfam<O, T, 4, 1, 1, 1>(FAM_TREE);
+    } else {
+        s.tree8 = kfam<O, T, 8, 1, 2, 1>(FAM_TREE);
+        s.tree4 = kfam<O, T, 4, 1, 2, 1>(FAM_TREE);
+    }
     s.chain8 = kchain<O, T, 8>();
     s.chain4 = kchain<O, T, 4>();
     if constexpr (sizeof(T) == 4) {
