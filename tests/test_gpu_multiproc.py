@@ -77,9 +77,9 @@ def test_executor_random_host_transport(world):
     pairs, count, root, exchange variant, device or host buffers) through the
     one-rank-per-process path; every rank's code and recvbuf against the
     oracle."""
-    reports = _launch(world, "host", "random", 240)
+    reports = _launch(world, "host", "random", 600)
     for rep in reports:
-        assert rep["checked"] >= 100
+        assert rep["checked"] == int(os.environ.get("MVX_MP_CASES", "120")), rep["checked"]
         assert not rep["fails"], rep["fails"][:5]
 
 
