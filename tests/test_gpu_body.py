@@ -1,4 +1,4 @@
-"""The body kernels (k_tree_body / k_chain_body, mvx_ops.hip): large aligned
+"""The body kernels (k_tree_body / k_chain_body, mvx_ops_kern.h): large aligned
 full trees and chains over 4 or 8 unfolded leaves run a lean loop at 2
 resident blocks per CU; everything else (a head or tail outside the 16-byte
 body, misaligned leaves, folded leaves, small launches, MVX_NO_BODY) runs
