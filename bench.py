@@ -66,6 +66,8 @@ def parse():
                          "Infinity Cache: the number is HBM-bound, not cache-bound)")
     ap.add_argument("--exchange", default="auto", choices=["auto", "p2p", "pipe", "pipe2", "pipe8", "coll"])
     ap.add_argument("--tune-steps", type=int, default=5)
+    ap.add_argument("--no-kernels", action="store_true",
+                    help="N = 1: skip the C3 / C4 / C5 combine-kernel rates after the timed region")
     ap.add_argument("--transport", default="rccl", choices=["rccl", "host"],
                     help="host: ranks may share a GPU, bytes move through gloo (a test of the "
                          "multi-GPU leg on a 1-GPU box; not a performance configuration)")
@@ -222,7 +224,24 @@ def run_single(args, mvx, dev):
     out["parity"] = parity
     if not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline_op(nbytes, args.cpu_seconds)
+    if not args.no_kernels:
+        out["combine_kernels"] = combine_kernels(mvx)
     print(json.dumps(out), flush=True)
+
+
+def combine_kernels(mvx):
+    """After the timed region: the combine kernel each rank of the
+    multi-GPU configs launches, at that config's shapes, alone on this GPU
+    (tools/bench_kernels.py: rotating buffer sets, HIP events on the launch
+    stream) -- C3 8-leaf SUM f32 tree over 32 MiB leaves, C4 4-leaf BAND int64
+    chain over 256 MiB, C5 8-leaf MAXLOC FLOAT_INT tree over 64 MiB."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import bench_kernels as BK
+    rows = [BK.run(mvx, "C3", MPI_SUM, MPI_FLOAT, 8, 0, 32 * MIB, 4, quiet=True),
+            BK.run(mvx, "C4", MPI_BAND, MPI_LONG, 4, 1, 256 * MIB, 2, quiet=True),
+            BK.run(mvx, "C5", MPI_MAXLOC, MPI_FLOAT_INT, 8, 0, 64 * MIB, 2, quiet=True)]
+    return [{k: r[k] for k in ("config", "kernel", "k", "alg_bytes_per_launch", "kernel_us", "hbm_frac")}
+            for r in rows]
 
 
 # ------------------------------------------------------------------ common --

@@ -26,7 +26,7 @@ MIB = 1 << 20
 PEAK = 8000.0
 
 
-def run(mvx, name, op, dtype, k, shape, leaf_bytes, sets, reps=20, warm=3):
+def run(mvx, name, op, dtype, k, shape, leaf_bytes, sets, reps=20, warm=3, quiet=False):
     import torch
     n_elems = leaf_bytes // mvx.dtype_info(dtype)[0]
     bufs = []
@@ -73,7 +73,8 @@ def run(mvx, name, op, dtype, k, shape, leaf_bytes, sets, reps=20, warm=3):
     out = {"config": name, "kernel": mvx.last_kernel(), "k": k, "leaf_bytes": leaf_bytes,
            "alg_bytes_per_launch": alg, "kernel_us": round(us, 2), "achieved_GBps": round(gbs, 1),
            "hbm_frac": round(gbs / PEAK, 4), "sets": sets}
-    print(json.dumps(out), flush=True)
+    if not quiet:
+        print(json.dumps(out), flush=True)
     del bufs
     torch.cuda.empty_cache()
     return out

@@ -26,13 +26,13 @@ fi
 if [[ $STAGE == all || $STAGE == pmc ]]; then
   # one counter set per pass (FETCH_SIZE takes 3 TCC counters, WRITE_SIZE 2)
   rm -rf gpurun_out/pmc_fetch gpurun_out/pmc_write
-  run timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o f -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/pmc_fetch.log 2>&1 || { tail -30 gpurun_out/pmc_fetch.log; exit 1; }
-  run timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o w -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/pmc_write.log 2>&1 || { tail -30 gpurun_out/pmc_write.log; exit 1; }
+  run timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o f -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-kernels > gpurun_out/pmc_fetch.log 2>&1 || { tail -30 gpurun_out/pmc_fetch.log; exit 1; }
+  run timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o w -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-kernels > gpurun_out/pmc_write.log 2>&1 || { tail -30 gpurun_out/pmc_write.log; exit 1; }
   python3 tools/pmc_summary.py gpurun_out/pmc_fetch gpurun_out/pmc_write "k_combine<2, float, 2, 4, 1, 0>" sum_f32_k2_nt 268435456 805306368 gpurun_out/pmc_c2.json || exit 1
 fi
 if [[ $STAGE == all || $STAGE == prof ]]; then
   rm -rf gpurun_out/prof_kt
-  run timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_kt -o kt -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/prof_kt.log 2>&1 || { tail -30 gpurun_out/prof_kt.log; exit 1; }
+  run timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_kt -o kt -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-kernels > gpurun_out/prof_kt.log 2>&1 || { tail -30 gpurun_out/prof_kt.log; exit 1; }
   find gpurun_out/prof_kt -name "*stats*"
 fi
 if [[ $STAGE == all || $STAGE == kernels ]]; then
