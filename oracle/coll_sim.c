@@ -100,10 +100,78 @@ static void tm_copy(void *dst, const void *src, long n, int dtype)
     }
 }
 
-static char *dup_buf(const void *src, long bytes)
+/* Data buffers (temporaries, snapshots) hold every byte the type map of
+ * their elements touches relative to the origin, [lo, hi): for a derived
+ * type whose map reaches past count * extent (e.g. displacements from 1 with
+ * extent 14 and map bytes up to 14) that is wider than count * extent --
+ * the bytes the reference's MPI_Sendrecv of the type moves and its
+ * MALLOC(count * extent) - lb temporaries hold.  The allocation's base is
+ * kept in a small table so data_free can find it from the origin. */
+typedef struct { long lo, hi; } span_t;
+
+static span_t span_of(int dtype, long n)
 {
-    char *b = (char *)malloc(bytes > 0 ? (size_t)bytes : 1);
-    if (bytes > 0) memcpy(b, src, (size_t)bytes);
+    int E, TS;
+    long nb, i, off, len;
+    span_t s = {0, 0};
+    if (orc_dtype_info(dtype, &E, &TS) || n <= 0) return s;
+    s.hi = n * E;
+    nb = orc_type_nblocks(dtype);
+    for (i = 0; i < nb; i++) {
+        if (orc_type_block(dtype, i, &off, &len)) continue;
+        if (off < s.lo) s.lo = off;
+        if ((n - 1) * E + off + len > s.hi) s.hi = (n - 1) * E + off + len;
+    }
+    return s;
+}
+
+#define DATA_SLOTS 8192
+static struct { char *origin, *base; } g_data[DATA_SLOTS];
+
+/* zeroed buffer for `bytes` (= n * extent) bytes of dtype; returns the origin */
+static char *data_calloc(long bytes, int dtype)
+{
+    int E, TS, i;
+    long n;
+    span_t s;
+    char *b;
+    orc_dtype_info(dtype, &E, &TS);
+    n = E > 0 ? bytes / E : 0;
+    s = span_of(dtype, n);
+    if (s.hi < bytes) s.hi = bytes;
+    b = (char *)calloc((size_t)(s.hi - s.lo) + 1, 1);
+    for (i = 0; i < DATA_SLOTS; i++)
+        if (!g_data[i].origin) {
+            g_data[i].origin = b - s.lo;
+            g_data[i].base = b;
+            return b - s.lo;
+        }
+    abort();      /* more live buffers than any schedule here needs */
+}
+
+static void data_free(void *origin)
+{
+    int i;
+    if (!origin) return;
+    for (i = 0; i < DATA_SLOTS; i++)
+        if (g_data[i].origin == origin) {
+            free(g_data[i].base);
+            g_data[i].origin = g_data[i].base = NULL;
+            return;
+        }
+    abort();
+}
+
+/* a snapshot of `bytes` (= n * extent) bytes of dtype at src: the whole span */
+static char *dup_buf(const void *src, long bytes, int dtype)
+{
+    int E, TS;
+    char *b = data_calloc(bytes, dtype);
+    span_t s;
+    orc_dtype_info(dtype, &E, &TS);
+    s = span_of(dtype, E > 0 ? bytes / E : 0);
+    if (s.hi < bytes) s.hi = bytes;
+    if (s.hi > s.lo) memcpy(b + s.lo, (const char *)src + s.lo, (size_t)(s.hi - s.lo));
     return b;
 }
 
@@ -136,10 +204,10 @@ static void uop_swapped(int op, int dtype, const void *theirs, void *mine, int l
     int E, TS;
     char *tmp;
     orc_dtype_info(dtype, &E, &TS);
-    tmp = dup_buf(theirs, (long)len * E);
+    tmp = dup_buf(theirs, (long)len * E, dtype);
     uop(op, dtype, mine, tmp, len, err);
     tm_copy(mine, tmp, len, dtype);
-    free(tmp);
+    data_free(tmp);
 }
 
 int orc_algorithm_op(int coll, int p, long total_count, int dtype, int op)
@@ -212,13 +280,13 @@ static char *smp_fold(int p, const void *const *send, int count, int dtype, int 
     char *tmp;
     orc_dtype_info(dtype, &E, &TS);
     bytes = (long)count * E;
-    tmp = (char *)calloc((size_t)bytes + 1, 1);
+    tmp = data_calloc(bytes, dtype);
     tm_copy(tmp, send[0], count, dtype);
     for (i = 1; i < p; i++) {
-        char *slot = (char *)calloc((size_t)bytes + 1, 1);
+        char *slot = data_calloc(bytes, dtype);
         tm_copy(slot, send[i], count, dtype);
         uop(op, dtype, slot, tmp, count, &dummy);
-        free(slot);
+        data_free(slot);
     }
     return tmp;
 }
@@ -258,7 +326,7 @@ int orc_allreduce(int p, const void *const *send, void *const *recv,
             else {
                 char *tmp = smp_fold(p, send, count, dtype, op);
                 tm_copy(recv[0], tmp, count, dtype);                       /* 5904-5906 */
-                free(tmp);
+                data_free(tmp);
                 for (r = 1; r < p; r++) tm_copy(recv[r], recv[0], count, dtype);  /* Bcast 5926 */
             }
             return 0;
@@ -279,9 +347,9 @@ int orc_allreduce(int p, const void *const *send, void *const *recv,
         if (r < 2 * rem) {
             if (r % 2 == 0) newrank[r] = -1;
             else {
-                char *tmp = dup_buf(recv[r - 1], bytes);
+                char *tmp = dup_buf(recv[r - 1], bytes, dtype);
                 uop(op, dtype, tmp, recv[r], count, &err[r]);
-                free(tmp);
+                data_free(tmp);
                 newrank[r] = r / 2;
             }
         } else newrank[r] = r - rem;
@@ -292,7 +360,7 @@ int orc_allreduce(int p, const void *const *send, void *const *recv,
     if (alg == ORC_ALG_RECDBL) {
         for (mask = 1; mask < pof2; mask <<= 1) {
             for (r = 0; r < p; r++)
-                if (newrank[r] != -1) snap[r] = dup_buf(recv[r], bytes);
+                if (newrank[r] != -1) snap[r] = dup_buf(recv[r], bytes, dtype);
             for (r = 0; r < p; r++) {
                 int dst;
                 if (newrank[r] == -1) continue;
@@ -300,7 +368,7 @@ int orc_allreduce(int p, const void *const *send, void *const *recv,
                 if (commute(op) || dst < r) uop(op, dtype, snap[dst], recv[r], count, &err[r]);
                 else uop_swapped(op, dtype, snap[dst], recv[r], count, &err[r]);
             }
-            for (r = 0; r < p; r++) { free(snap[r]); snap[r] = NULL; }
+            for (r = 0; r < p; r++) { data_free(snap[r]); snap[r] = NULL; }
         }
     } else {
         int *cnts = (int *)malloc(sizeof(int) * (size_t)pof2);
@@ -329,7 +397,7 @@ int orc_allreduce(int p, const void *const *send, void *const *recv,
                     ridx[r] = sidx[r] + pof2 / (mask * 2);
                     for (i = ridx[r]; i < lidx[r]; i++) rcnt[r] += cnts[i];
                 }
-                snap[r] = dup_buf(recv[r], bytes);
+                snap[r] = dup_buf(recv[r], bytes, dtype);
             }
             for (r = 0; r < p; r++) {
                 int dst;
@@ -341,7 +409,7 @@ int orc_allreduce(int p, const void *const *send, void *const *recv,
                     rcnt[r], &err[r]);
             }
             for (r = 0; r < p; r++) {
-                free(snap[r]); snap[r] = NULL;
+                data_free(snap[r]); snap[r] = NULL;
                 if (newrank[r] == -1) continue;
                 sidx[r] = ridx[r];
                 if ((mask << 1) < pof2) lidx[r] = ridx[r] + pof2 / (mask << 1);
@@ -362,7 +430,7 @@ int orc_allreduce(int p, const void *const *send, void *const *recv,
                     ridx[r] = sidx[r] - pof2 / (mask * 2);
                     for (i = ridx[r]; i < sidx[r]; i++) rcnt[r] += cnts[i];
                 }
-                snap[r] = dup_buf(recv[r], bytes);
+                snap[r] = dup_buf(recv[r], bytes, dtype);
             }
             for (r = 0; r < p; r++) {
                 int dst;
@@ -373,7 +441,7 @@ int orc_allreduce(int p, const void *const *send, void *const *recv,
                 tm_copy((char *)recv[r] + off, snap[dst] + off, rcnt[r], dtype);
             }
             for (r = 0; r < p; r++) {
-                free(snap[r]); snap[r] = NULL;
+                data_free(snap[r]); snap[r] = NULL;
                 if (newrank[r] == -1) continue;
                 if (newrank[r] > (newrank[r] ^ mask)) sidx[r] = ridx[r];
             }
@@ -421,7 +489,7 @@ int orc_reduce(int p, const void *const *send, void *const *recv,
                  * otherwise it sends tmpbuf to root (5168-5171, 5179-5181) */
                 char *tmp = smp_fold(p, send, count, dtype, op);
                 tm_copy(recv[root], tmp, count, dtype);
-                free(tmp);
+                data_free(tmp);
             }
             return 0;
         }
@@ -433,7 +501,7 @@ int orc_reduce(int p, const void *const *send, void *const *recv,
     snap = (char **)calloc((size_t)p, sizeof(char *));
     /* non-roots reduce into a private buffer (4590-4594) */
     for (r = 0; r < p; r++) {
-        wb[r] = (r == root) ? (char *)recv[r] : (char *)calloc((size_t)bytes, 1);
+        wb[r] = (r == root) ? (char *)recv[r] : data_calloc(bytes, dtype);
         tm_copy(wb[r], send[r], count, dtype);
     }
     pof2 = pof2_lgn(p, &lgn);
@@ -457,9 +525,9 @@ int orc_reduce(int p, const void *const *send, void *const *recv,
             if (r < 2 * rem) {
                 if (r % 2 != 0) newrank[r] = -1;
                 else {
-                    char *tmp = dup_buf(wb[r + 1], bytes);
+                    char *tmp = dup_buf(wb[r + 1], bytes, dtype);
                     uop(op, dtype, tmp, wb[r], count, &err[r]);
-                    free(tmp);
+                    data_free(tmp);
                     newrank[r] = r / 2;
                 }
             } else newrank[r] = r - rem;
@@ -483,7 +551,7 @@ int orc_reduce(int p, const void *const *send, void *const *recv,
                     ridx[r] = sidx[r] + pof2 / (mask * 2);
                     for (i = ridx[r]; i < lidx[r]; i++) rcnt[r] += cnts[i];
                 }
-                snap[r] = dup_buf(wb[r], bytes);
+                snap[r] = dup_buf(wb[r], bytes, dtype);
             }
             for (r = 0; r < p; r++) {
                 int dst;
@@ -494,7 +562,7 @@ int orc_reduce(int p, const void *const *send, void *const *recv,
                 uop(op, dtype, snap[dst] + off, wb[r] + off, rcnt[r], &err[r]);
             }
             for (r = 0; r < p; r++) {
-                free(snap[r]); snap[r] = NULL;
+                data_free(snap[r]); snap[r] = NULL;
                 if (newrank[r] == -1) continue;
                 sidx[r] = ridx[r];
                 if ((mask << 1) < pof2) lidx[r] = ridx[r] + pof2 / (mask << 1);
@@ -547,7 +615,7 @@ int orc_reduce(int p, const void *const *send, void *const *recv,
                 peer[r] = dst;
             }
             for (r = 0; r < p; r++)
-                if (active[r]) snap[r] = dup_buf(wb[r], bytes);
+                if (active[r]) snap[r] = dup_buf(wb[r], bytes, dtype);
             for (r = 0; r < p; r++) {
                 long off;
                 if (!active[r] || sender[r]) continue;
@@ -555,7 +623,7 @@ int orc_reduce(int p, const void *const *send, void *const *recv,
                 tm_copy(wb[r] + off, snap[peer[r]] + off, rcnt[r], dtype);
             }
             for (r = 0; r < p; r++) {
-                free(snap[r]); snap[r] = NULL;
+                data_free(snap[r]); snap[r] = NULL;
                 if (!active[r]) continue;
                 if (sender[r]) { active[r] = 0; continue; }
                 if (newrank[r] > (newrank[r] ^ mask)) sidx[r] = ridx[r];
@@ -584,20 +652,20 @@ int orc_reduce(int p, const void *const *send, void *const *recv,
             }
             for (r = 0; r < p; r++)
                 if (recv_from[r] >= 0)
-                    snap[recv_from[r]] = dup_buf(wb[recv_from[r]], bytes);
+                    snap[recv_from[r]] = dup_buf(wb[recv_from[r]], bytes, dtype);
             for (r = 0; r < p; r++) {
                 if (recv_from[r] < 0) continue;
                 if (commute(op)) uop(op, dtype, snap[recv_from[r]], wb[r], count, &err[r]);
                 else uop_swapped(op, dtype, snap[recv_from[r]], wb[r], count, &err[r]);
             }
-            for (r = 0; r < p; r++) { free(snap[r]); snap[r] = NULL; }
+            for (r = 0; r < p; r++) { data_free(snap[r]); snap[r] = NULL; }
             free(recv_from);
         }
         if (lroot != root) tm_copy(wb[root], wb[0], count, dtype);
     }
     for (r = 0; r < p; r++) {
         rc[r] = err[r];
-        if (r != root) free(wb[r]);
+        if (r != root) data_free(wb[r]);
     }
     free(err); free(wb); free(snap);
     return 0;
@@ -649,8 +717,8 @@ static void rs_recdbl(int p, const void *const *send, void *const *recv,
     dtr = (int *)calloc((size_t)p, sizeof(int));
     mtr = (int *)calloc((size_t)p, sizeof(int));
     for (r = 0; r < p; r++) {
-        res[r] = (char *)calloc((size_t)bytes + 1, 1);
-        tmp[r] = (char *)calloc((size_t)bytes + 1, 1);
+        res[r] = data_calloc(bytes, dtype);
+        tmp[r] = data_calloc(bytes, dtype);
         tm_copy(res[r], send[r], total, dtype);
     }
     for (mask = 1, i = 0; mask < p; mask <<= 1, i++) {
@@ -662,19 +730,19 @@ static void rs_recdbl(int p, const void *const *send, void *const *recv,
         }
         /* the exchange: rank r receives dst's tmp_results minus r's
          * partner subtree (dst's sendtype = r's recvtype) */
-        for (r = 0; r < p; r++) snap[r] = dup_buf(res[r], bytes);
+        for (r = 0; r < p; r++) snap[r] = dup_buf(res[r], bytes, dtype);
         for (r = 0; r < p; r++) {
             const int dst = r ^ mask;
             if (dst >= p) continue;
             copy_two(tmp[r], snap[dst], except_subtree(recvcnts, p, dtr[r], mask), E, dtype);
             received[r] = 1;
         }
-        for (r = 0; r < p; r++) { free(snap[r]); snap[r] = NULL; }
+        for (r = 0; r < p; r++) { data_free(snap[r]); snap[r] = NULL; }
         /* forwarding inside subtrees that had no partner */
         for (kk = mask, k = 0; kk; kk >>= 1) k++;
         k--;
         for (tmask = mask >> 1; tmask; tmask >>= 1, k--) {
-            for (r = 0; r < p; r++) snap[r] = dup_buf(tmp[r], bytes);
+            for (r = 0; r < p; r++) snap[r] = dup_buf(tmp[r], bytes, dtype);
             for (r = 0; r < p; r++) {
                 int dst = r ^ tmask, tree_root, done;
                 if (dtr[r] + mask <= p) continue;
@@ -685,7 +753,7 @@ static void rs_recdbl(int p, const void *const *send, void *const *recv,
                     received[r] = 1;
                 }
             }
-            for (r = 0; r < p; r++) { free(snap[r]); snap[r] = NULL; }
+            for (r = 0; r < p; r++) { data_free(snap[r]); snap[r] = NULL; }
         }
         /* the combine, over the two runs of the recvtype */
         for (r = 0; r < p; r++) {
@@ -704,7 +772,7 @@ static void rs_recdbl(int p, const void *const *send, void *const *recv,
     }
     for (r = 0; r < p; r++) {
         if (recvcnts[r]) tm_copy(recv[r], res[r] + (long)disps[r] * E, recvcnts[r], dtype);
-        free(res[r]); free(tmp[r]);
+        data_free(res[r]); data_free(tmp[r]);
     }
     free(res); free(tmp); free(snap); free(received); free(dtr); free(mtr);
 }
@@ -741,16 +809,16 @@ int orc_reduce_scatter(int p, const void *const *send, void *const *recv,
         int *lidx = (int *)calloc((size_t)p, sizeof(int));
         int *rcnt = (int *)calloc((size_t)p, sizeof(int));
         for (r = 0; r < p; r++) {
-            res[r] = (char *)calloc((size_t)bytes, 1);
+            res[r] = data_calloc(bytes, dtype);
             tm_copy(res[r], send[r], total, dtype);
         }
         for (r = 0; r < p; r++) {
             if (r < 2 * rem) {
                 if (r % 2 == 0) newrank[r] = -1;
                 else {
-                    char *tmp = dup_buf(res[r - 1], bytes);
+                    char *tmp = dup_buf(res[r - 1], bytes, dtype);
                     uop(op, dtype, tmp, res[r], total, &err[r]);
-                    free(tmp);
+                    data_free(tmp);
                     newrank[r] = r / 2;
                 }
             } else newrank[r] = r - rem;
@@ -777,7 +845,7 @@ int orc_reduce_scatter(int p, const void *const *send, void *const *recv,
                     ridx[r] = sidx[r] + mask;
                     for (i = ridx[r]; i < lidx[r]; i++) rcnt[r] += newcnts[i];
                 }
-                snap[r] = dup_buf(res[r], bytes);
+                snap[r] = dup_buf(res[r], bytes, dtype);
             }
             for (r = 0; r < p; r++) {
                 int nd, dst;
@@ -790,7 +858,7 @@ int orc_reduce_scatter(int p, const void *const *send, void *const *recv,
                     uop(op, dtype, snap[dst] + off, res[r] + off, rcnt[r], &err[r]);
             }
             for (r = 0; r < p; r++) {
-                free(snap[r]); snap[r] = NULL;
+                data_free(snap[r]); snap[r] = NULL;
                 if (newrank[r] == -1) continue;
                 sidx[r] = ridx[r];
                 lidx[r] = ridx[r] + mask;
@@ -802,7 +870,7 @@ int orc_reduce_scatter(int p, const void *const *send, void *const *recv,
         for (r = 0; r < 2 * rem; r += 2)
             if (recvcnts[r])
                 tm_copy(recv[r], res[r + 1] + (long)disps[r] * E, recvcnts[r], dtype);
-        for (r = 0; r < p; r++) free(res[r]);
+        for (r = 0; r < p; r++) data_free(res[r]);
         free(res); free(snap); free(newrank); free(newcnts); free(newdisps);
         free(sidx); free(ridx); free(lidx); free(rcnt);
     } else if (alg == ORC_ALG_RS_PAIRWISE) {
@@ -814,11 +882,11 @@ int orc_reduce_scatter(int p, const void *const *send, void *const *recv,
             for (i = 1; i < p; i++) {
                 int src = (r - i + p) % p;
                 long n = recvcnts[r];
-                char *tmp = (char *)calloc((size_t)(n * E + 1), 1);
+                char *tmp = data_calloc(n * E, dtype);
                 tm_copy(tmp, (const char *)send[src] + (long)disps[r] * E, n, dtype);
                 if (commute(op) || src < r) uop(op, dtype, tmp, recv[r], recvcnts[r], &err[r]);
                 else uop_swapped(op, dtype, tmp, recv[r], recvcnts[r], &err[r]);
-                free(tmp);
+                data_free(tmp);
             }
         }
     } else {
@@ -850,11 +918,11 @@ int orc_scan(int p, const void *const *send, void *const *recv, int count,
     snap = (char **)calloc((size_t)p, sizeof(char *));
     for (r = 0; r < p; r++) {
         tm_copy(recv[r], send[r], count, dtype);
-        partial[r] = (char *)calloc((size_t)bytes, 1);
+        partial[r] = data_calloc(bytes, dtype);
         tm_copy(partial[r], send[r], count, dtype);
     }
     for (mask = 1; mask < p; mask <<= 1) {
-        for (r = 0; r < p; r++) snap[r] = dup_buf(partial[r], bytes);
+        for (r = 0; r < p; r++) snap[r] = dup_buf(partial[r], bytes, dtype);
         for (r = 0; r < p; r++) {
             int dst = r ^ mask, dummy = 0;
             if (dst >= p) continue;
@@ -867,9 +935,9 @@ int orc_scan(int p, const void *const *send, void *const *recv, int count,
                 uop_swapped(op, dtype, snap[dst], partial[r], count, &dummy);
             }
         }
-        for (r = 0; r < p; r++) { free(snap[r]); snap[r] = NULL; }
+        for (r = 0; r < p; r++) { data_free(snap[r]); snap[r] = NULL; }
     }
-    for (r = 0; r < p; r++) free(partial[r]);
+    for (r = 0; r < p; r++) data_free(partial[r]);
     free(partial); free(snap);
     return 0;
 }

@@ -226,7 +226,7 @@ def _op_case(rng):
                 sio=int(rng.random() < 0.3), seed=int(rng.integers(1 << 30)))
 
 
-@pytest.mark.parametrize("batch", range(4))
+@pytest.mark.parametrize("batch", range(int(os.environ.get("MVX_FUZZ_OP_BATCHES", "4"))))
 def test_random_op_functions(mvx, oracle, batch):
     """The predefined ops through their MPI_User_function symbols (MPIR_SUM
     ...) on random sizes (up to ~90 MiB), operand kinds (HBM, pageable,

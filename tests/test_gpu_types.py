@@ -236,7 +236,7 @@ def test_struct_collectives_smp_flavour(mvx, oracle, types, where, p, tname, op,
             mvx.MPI_Op_free(uop)
 
 
-@pytest.mark.parametrize("batch", range(3))
+@pytest.mark.parametrize("batch", range(int(__import__("os").environ.get("MVX_FUZZ_DT_BATCHES", "3"))))
 def test_random_derived_sweep(mvx, oracle, types, batch):
     """Seeded random cases over the derived types above: collective, p,
     count, root, ragged recvcnts, exchange variant, device or host buffers,
@@ -266,10 +266,15 @@ def test_random_derived_sweep(mvx, oracle, types, batch):
             cnts = [max(0, n // p + int(rng.integers(-1, 2))) for _ in range(p)] if coll == "rs" else None
             tot = sum(cnts) if cnts else n
             kind = {"st_di": "di", "st_fi": "fi", "vec_st": None}.get(tname)
-            S = [(_pairs_bytes(h, tot, ext, int(rng.integers(1 << 30)), kind) if kind
-                  else rng.integers(0, 256, max(tot * ext, 1), dtype=np.uint8)) for _ in range(p)]
+            # buffers cover the type map's span: a type whose map reaches past
+            # its extent (hidx_chr: lb 1, extent 14, map up to byte 15) touches
+            # bytes past count * extent -- the caller's to provide, as in MPI
+            tail = 64
+            S = [np.concatenate([(_pairs_bytes(h, tot, ext, int(rng.integers(1 << 30)), kind) if kind
+                                  else rng.integers(0, 256, tot * ext, dtype=np.uint8)),
+                                 rng.integers(0, 256, tail, dtype=np.uint8)]) for _ in range(p)]
             nrecv = [(cnts[r] if cnts else tot) for r in range(p)]
-            R0 = [np.full(max(k, 1) * ext, 0x5C, np.uint8) for k in nrecv]
+            R0 = [np.full(k * ext + tail, 0x5C, np.uint8) for k in nrecv]
             where = str(rng.choice(["device", "host"]))
             if where == "device":
                 sends = [torch.from_numpy(s).cuda() for s in S]
