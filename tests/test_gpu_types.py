@@ -246,9 +246,14 @@ def test_random_derived_sweep(mvx, oracle, types, batch):
     outside the type map keep the caller's pattern."""
     import torch
     rng = np.random.default_rng(9000 + batch)
+    # plus a type whose map starts before its origin (lb -8): buffers get a
+    # head margin too, and the calls take origins inside them
+    types = dict(types)
+    types["hidx_neg"] = _both(mvx, oracle, "hindexed", 2, [1, 1], [-8, 4], I)
     names = sorted(types)
     comms = {}
     checked = undefined = 0
+    head = 64
     try:
         for _ in range(30):
             tname = str(rng.choice(names))
@@ -270,11 +275,12 @@ def test_random_derived_sweep(mvx, oracle, types, batch):
             # its extent (hidx_chr: lb 1, extent 14, map up to byte 15) touches
             # bytes past count * extent -- the caller's to provide, as in MPI
             tail = 64
-            S = [np.concatenate([(_pairs_bytes(h, tot, ext, int(rng.integers(1 << 30)), kind) if kind
+            S = [np.concatenate([rng.integers(0, 256, head, dtype=np.uint8),
+                                 (_pairs_bytes(h, tot, ext, int(rng.integers(1 << 30)), kind) if kind
                                   else rng.integers(0, 256, tot * ext, dtype=np.uint8)),
                                  rng.integers(0, 256, tail, dtype=np.uint8)]) for _ in range(p)]
             nrecv = [(cnts[r] if cnts else tot) for r in range(p)]
-            R0 = [np.full(k * ext + tail, 0x5C, np.uint8) for k in nrecv]
+            R0 = [np.full(head + k * ext + tail, 0x5C, np.uint8) for k in nrecv]
             where = str(rng.choice(["device", "host"]))
             if where == "device":
                 sends = [torch.from_numpy(s).cuda() for s in S]
@@ -283,9 +289,10 @@ def test_random_derived_sweep(mvx, oracle, types, batch):
                 sends = [s.copy() for s in S]
                 recvs = [r.copy() for r in R0]
             root = int(rng.integers(0, p))
-            r, rcs = _coll(comm, coll, sends, recvs, tot, h, op, root, cnts)
+            r, rcs = _coll(comm, coll, [x[head:] for x in sends], [x[head:] for x in recvs], tot, h, op, root,
+                           cnts)
             ref = [x.copy() for x in R0]
-            rref = _oracle(oracle, coll, S, ref, tot, h, op, root, cnts)
+            rref = _oracle(oracle, coll, [x[head:] for x in S], [x[head:] for x in ref], tot, h, op, root, cnts)
             case = (tname, op, p, coll, n, cnts, mode, where, root)
             if r == mvx.MPI_ERR_TYPE:        # the documented refusal (MAXLOC, extent != pair struct)
                 continue
@@ -300,3 +307,4 @@ def test_random_derived_sweep(mvx, oracle, types, batch):
     finally:
         for c in comms.values():
             c.free()
+        assert mvx.MPI_Type_free(types["hidx_neg"])[0] == 0 and oracle.type_free(types["hidx_neg"]) == 0
