@@ -453,7 +453,10 @@ def run_multi(args, mvx, dev, world, rank, local):
         t[0] = time.perf_counter() - t0
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         tried[name] = {"ms_per_step": round(float(t.item()) * 1e3 / args.tune_steps, 4), "parity": ok}
-    choice = min(names, key=lambda k: tried[k]["ms_per_step"])
+    # the fastest variant whose parity did not fail (a MISMATCH stays on
+    # record in exchange_tuning but is never the one timed)
+    ok_names = [k for k in names if tried[k]["parity"] is not False] or names
+    choice = min(ok_names, key=lambda k: tried[k]["ms_per_step"])
     box = [choice]
     dist.broadcast_object_list(box, src=0)
     choice = box[0]
