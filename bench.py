@@ -57,6 +57,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true",
                     help="skip the CPU leg (and with it the parity check against it)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--prewarm-ms", type=float, default=0.0,
+                    help="N = 1: untimed back-to-back steps for this long before the W warmup steps "
+                         "(0 = none); reported in the line")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r02", "pmc_c2.json"),
                     help="committed rocprofv3 PMC summary for the traffic field")
     ap.add_argument("--block-cap", type=int, default=0)
@@ -184,6 +187,27 @@ def load_traffic(path, kernel_tag, kernel_symbol, nbytes):
     return d.get("hbm_bytes_per_launch"), os.path.relpath(path, ROOT)
 
 
+def prewarm(args, step):
+    """Untimed, before the W warmup steps: back-to-back steps for
+    --prewarm-ms of wall time, so the timed steps do not start on a GPU
+    still raising its clocks (a 5-step warmup is < 1 ms of work).  Reported
+    in the line as "prewarm"."""
+    import torch
+    if args.prewarm_ms <= 0:
+        return None
+    n, t0 = 0, time.perf_counter()
+    while True:
+        for _ in range(8):
+            step()
+        n += 8
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        if dt * 1e3 >= args.prewarm_ms:
+            break
+    return {"steps": n, "ms": round(dt * 1e3, 1),
+            "note": "untimed steps before the W warmup steps (clock ramp-up); not in value"}
+
+
 def run_single(args, mvx, dev):
     import torch
     nbytes = (args.mib or 256) * MIB
@@ -191,8 +215,8 @@ def run_single(args, mvx, dev):
     stream = torch.cuda.current_stream()
     x_in = [synth_f32(n, 0x9E3779B9 ^ (2 * s * 1000003 + 1), dev) for s in range(args.sets)]
     x_io = [synth_f32(n, 0x9E3779B9 ^ ((2 * s + 1) * 1000003 + 1), dev) for s in range(args.sets)]
-    # cpu_baseline leg, part 1: the reference op on the same inputs (checker)
-    parity = None if args.no_cpu_baseline else parity_op(mvx, x_in[0], x_io[0], n, stream)
+    # the parity check reads set 0 before any step has touched it
+    keep = None if args.no_cpu_baseline else (x_in[0].clone(), x_io[0].clone())
     it = [0]
 
     def step():
@@ -202,7 +226,15 @@ def run_single(args, mvx, dev):
         if rc:
             raise RuntimeError("mvx_op_apply rc=%d" % rc)
 
+    # from input synthesis to the last timed step the GPU never idles: the
+    # host-side parity check and the CPU leg run after the timed region
+    warm = prewarm(args, step)
     times = timed(args, step, stream, 1)
+    # cpu_baseline leg, part 1: the reference op on the same inputs (checker)
+    parity = None
+    if keep is not None:
+        parity = parity_op(mvx, keep[0], keep[1], n, stream)
+        del keep
     kernel = mvx.last_kernel()
     symbol = mvx.last_kernel_symbol()
     kern_s = times["dev_ms"] / 1e3 / args.steps           # HIP events on the launch stream
@@ -222,6 +254,7 @@ def run_single(args, mvx, dev):
                   "vector_bytes_per_rank": nbytes, "op": "MPI_SUM", "datatype": "MPI_FLOAT",
                   "parallelism": "single GPU"}, roof)
     out["parity"] = parity
+    out["prewarm"] = warm
     if not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline_op(nbytes, args.cpu_seconds)
     if not args.no_kernels:

@@ -17,7 +17,11 @@
 //   MPI_Type_struct      type_struct.c:106-330 (ALIGNMENT_VALUE 0: the x86-64
 //                        "largest member" struct layout, util/structlayout.c)
 //   MPI_Type_commit      type_commit.c:41-143 (dense structs become is_contig)
-//   MPI_Type_free        type_free.c:60-105
+//   MPI_Type_free        type_free.c:60-105, with the reference counts of
+//                        MPIR_Type_dup / MPIR_Type_free (type_util.c:29-130):
+//                        a type holds a reference on every derived type it
+//                        was built from, so freeing a member first leaves it
+//                        in place (handle and all) until its last user goes
 // Basic and pair handles are as MPIR_Init_dtes registers them
 // (initdte.c:106-280, MPIR_Setup_base_datatype 281-310).
 #include <hip/hip_runtime.h>
@@ -36,7 +40,7 @@ namespace dt {
 struct Blk { long off, len; };
 
 struct Type {
-    int used, kind, old, count, is_contig, has_lb, has_ub, no_old;
+    int used, ref, kind, old, count, is_contig, has_lb, has_ub, no_old;
     long align, extent, size, lb, ub, real_lb, real_ub;
     // STRUCT members (type_commit's contiguity test)
     std::vector<long> indices;
@@ -140,11 +144,47 @@ static int is_dense(const Type &t)
     return 0;
 }
 
+// MPIR_Type_dup (type_util.c:29-34): one more reference on a derived type
+// (basic and pair handles are permanent and never freed)
+static void retain(int h)
+{
+    if (Type *t = slot(h)) ++t->ref;
+}
+
+// MPIR_Type_free (type_util.c:56-130): drop one reference; the last one
+// frees the slot and, in turn, the references it held -- the old type
+// (default case, :97-99) or every struct member (MPIR_Free_struct_internals,
+// :226-236)
+static void release(int h)
+{
+    Type *t = slot(h);
+    if (!t) return;
+    if (t->ref > 1) { --t->ref; return; }
+    const int kind = t->kind, old = t->old;
+    const std::vector<int> members = t->types;
+    reset(*t);
+    if (kind == K_STRUCT) {
+        for (int m : members) release(m);
+    } else {
+        release(old);
+    }
+}
+
+// a new type with one reference (the caller's), holding a reference on
+// each derived type it was built from: its old type (type_contig.c:107,
+// 140, 144; type_hvec.c:110; type_hind.c:115) or its members
+// (type_struct.c:208)
 static int store(Type &n, int *newtype)
 {
     for (int i = 0; i < MVX_TYPE_DERIVED_MAX; ++i) {
         if (g_t[i].used) continue;
         n.used = 1;
+        n.ref = 1;
+        if (n.kind == K_STRUCT) {
+            for (int m : n.types) retain(m);
+        } else {
+            retain(n.old);
+        }
         g_t[i] = n;
         *newtype = MVX_TYPE_DERIVED_BASE + i;
         return MPI_SUCCESS;
@@ -616,7 +656,7 @@ extern "C" int mvx_type_free(int *type)
         if (*type != MPI_DATATYPE_NULL && basic(*type, v)) return MVX_ERR_PERM_TYPE;
         return MVX_ERR_TYPE_NULL;
     }
-    reset(*t);
+    release(*type);
     *type = MPI_DATATYPE_NULL;
     return MPI_SUCCESS;
 }

@@ -12,6 +12,9 @@
  *                        the x86-64 struct layout is "largest member",
  *                        util/structlayout.c)
  *   orc_type_commit      src/pt2pt/type_commit.c:41-143
+ *   orc_type_free        src/pt2pt/type_free.c:60-105 with the reference
+ *                        counts of MPIR_Type_dup / MPIR_Type_free
+ *                        (type_util.c:29-130, 226-236)
  * Basic types as MPIR_Setup_base_datatype (initdte.c:281-310: lb 0, ub = size,
  * align = size, real_lb = real_ub = 0) and the pair structs of
  * MPIR_Init_dtes (169-222: struct {value, int} with an MPI_UB at sizeof).
@@ -32,7 +35,7 @@
 enum { KB = 0, KC, KHV, KHI, KS, KUB, KLB };
 
 typedef struct {
-    int used, kind, old, count, is_contig, no_old, has_lb, has_ub;
+    int used, ref, kind, old, count, is_contig, no_old, has_lb, has_ub;
     long align, extent, size, lb, ub, real_lb, real_ub;
     long nmap, *moff, *mlen;       /* one element's type map, merged */
     int nmem, *mtype, *mblk;       /* struct members (commit's test) */
@@ -113,12 +116,44 @@ static int map_copies(dtype_t *n, const dtype_t *o, long base, long reps)
     return 0;
 }
 
+/* MPIR_Type_dup, type_util.c:29-34 */
+static void retain(int h)
+{
+    dtype_t *d = derived(h);
+    if (d) d->ref++;
+}
+
+/* MPIR_Type_free, type_util.c:56-130: the last reference frees the type and
+   the references it holds (old type :97-99, struct members :226-236) */
+static void release(int h)
+{
+    dtype_t *t = derived(h);
+    int i, kind, old, nmem, *mtype;
+    if (!t) return;
+    if (t->ref > 1) { t->ref--; return; }
+    kind = t->kind; old = t->old; nmem = t->nmem; mtype = t->mtype;
+    free(t->moff); free(t->mlen); free(t->mblk); free(t->midx);
+    memset(t, 0, sizeof *t);
+    if (kind == KS) {
+        for (i = 0; i < nmem; i++) release(mtype[i]);
+    } else {
+        release(old);
+    }
+    free(mtype);
+}
+
 static int store(dtype_t *n, int *newtype)
 {
-    int i;
+    int i, j;
     for (i = 0; i < DT_MAX; i++) {
         if (g_t[i].used) continue;
         n->used = 1;
+        n->ref = 1;
+        if (n->kind == KS) {
+            for (j = 0; j < n->nmem; j++) retain(n->mtype[j]);
+        } else {
+            retain(n->old);
+        }
         g_t[i] = *n;
         *newtype = DT_BASE + i;
         return 0;
@@ -375,10 +410,8 @@ int orc_type_commit(int h)
 
 int orc_type_free(int *h)
 {
-    dtype_t *t = derived(*h);
-    if (!t) return 3 | (5 << 6);
-    free(t->moff); free(t->mlen); free(t->mtype); free(t->mblk); free(t->midx);
-    memset(t, 0, sizeof *t);
+    if (!derived(*h)) return 3 | (5 << 6);
+    release(*h);
     *h = 0;
     return 0;
 }

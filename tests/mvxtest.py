@@ -46,8 +46,15 @@ def rand_vec(dtype, n, seed):
 
 def _rand_scalar(dt, n, rng):
     if dt.kind == "c":
+        # lane-wise: `re + 1j*im` would turn an inf / NaN imaginary draw into
+        # a NaN real lane too (1j*inf = nan+infj), so special values land
+        # only in the lane they were drawn for
         ft = np.dtype(np.float32 if dt.itemsize == 8 else np.float64)
-        return (_rand_scalar(ft, n, rng) + 1j * _rand_scalar(ft, n, rng)).astype(dt)
+        out = np.empty(n, dt)
+        lanes = out.view(ft)
+        lanes[0::2] = _rand_scalar(ft, n, rng)
+        lanes[1::2] = _rand_scalar(ft, n, rng)
+        return out
     if dt.kind == "f":
         v = rng.standard_normal(n) * np.exp2(rng.integers(-20, 20, n))
         v = np.where(rng.random(n) < 0.25, rng.integers(-3, 4, n), v)   # ties and zeros

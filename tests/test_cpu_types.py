@@ -193,3 +193,61 @@ def test_layout_and_density(mvx):
     assert mvx.hip().mvx_op_apply(mvx.MPI_MINLOC, c, None, None, 0, None) == 329
     for h in (v, s, f, c):
         mvx.MPI_Type_free(h)
+
+
+def _describe(mvx, h):
+    return (mvx.MPI_Type_extent(h)[1], mvx.MPI_Type_size(h)[1], mvx.MPI_Type_lb(h)[1], mvx.MPI_Type_ub(h)[1])
+
+
+def _describe_orc(oracle, h):
+    rc, lb, ub, ext, size = oracle.type_bounds(h)
+    assert rc == 0
+    return (ext, size, lb, ub)
+
+
+def test_free_keeps_types_others_were_built_from(mvx, oracle):
+    """MPI_Type_free on a type another type was built from only drops a
+    reference (MPIR_Type_dup / MPIR_Type_free, type_util.c:29-130): the
+    member stays in place until its last user is freed, so (1) committing a
+    struct after freeing a member, and (2) building over a contiguous type
+    whose old type was freed -- with another type created in between --
+    both see the original layout.  Product and oracle hand out the same
+    handles throughout."""
+    I, D = mvx.MPI_INT, mvx.MPI_DOUBLE
+
+    def both(ctor, *a):
+        r1 = getattr(mvx, "MPI_Type_" + ctor)(*a)
+        r2 = getattr(oracle, "type_" + ctor)(*a)
+        assert r1 == r2, (ctor, a, r1, r2)
+        assert r1[0] == 0
+        return r1[1]
+
+    def free(h):
+        assert mvx.MPI_Type_free(h) == (0, 0)
+        assert oracle.type_free(h) == 0
+
+    # (1) struct([contig(2, INT), INT]) -> free the member -> commit
+    c = both("contiguous", 2, I)
+    s = both("struct", 2, [1, 1], [0, 8], [c, I])
+    free(c)
+    other = both("contiguous", 5, D)            # must not reuse c's slot
+    assert other != c
+    assert mvx.MPI_Type_commit(s) == 0 and oracle.type_commit(s) == 0
+    assert _describe(mvx, s) == _describe_orc(oracle, s) == (12, 12, 0, 12)
+    assert mvx.type_layout(s)["dense"] == 1
+    # (2) contig(2, contig(3, dense struct)) after the struct is freed
+    ds = both("struct", 2, [1, 1], [0, 4], [I, mvx.MPI_FLOAT])
+    assert mvx.MPI_Type_commit(ds) == 0 and oracle.type_commit(ds) == 0
+    t3 = both("contiguous", 3, ds)
+    free(ds)
+    other2 = both("vector", 2, 1, 3, D)
+    assert other2 != ds
+    t6 = both("contiguous", 2, t3)
+    assert _describe(mvx, t6) == _describe_orc(oracle, t6) == (48, 48, 0, 48)
+    # the last reference frees the chain: every slot is reusable afterwards
+    for h in (t6, t3, s, other, other2):
+        free(h)
+    again = [both("contiguous", 1, I) for _ in range(3)]
+    assert sorted(again)[0] == min(c, s, ds, t3)
+    for h in again:
+        free(h)

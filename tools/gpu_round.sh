@@ -20,7 +20,8 @@ if [[ $STAGE == all || $STAGE == test ]]; then
   tail -3 gpurun_out/pytest_gpu.log
 fi
 if [[ $STAGE == all || $STAGE == bench ]]; then
-  run timeout -k 10 400 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || { tail -30 gpurun_out/bench.err; exit 1; }
+  # the driver's own command
+  run timeout -k 10 400 python3 bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/bench.json 2> gpurun_out/bench.err || { tail -30 gpurun_out/bench.err; exit 1; }
   cat gpurun_out/bench.json
 fi
 if [[ $STAGE == all || $STAGE == pmc ]]; then
@@ -32,8 +33,11 @@ if [[ $STAGE == all || $STAGE == pmc ]]; then
 fi
 if [[ $STAGE == all || $STAGE == prof ]]; then
   rm -rf gpurun_out/prof_kt
-  run timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_kt -o kt -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-kernels > gpurun_out/prof_kt.log 2>&1 || { tail -30 gpurun_out/prof_kt.log; exit 1; }
+  # the driver's own command under the kernel trace; every dispatch of the
+  # C2 kernel in order (prewarm / warmup / timed / evented / parity)
+  run timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_kt -o kt -- python3 bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/prof_kt.log 2>&1 || { tail -30 gpurun_out/prof_kt.log; exit 1; }
   find gpurun_out/prof_kt -name "*stats*"
+  python3 tools/dispatch_series.py gpurun_out/prof_kt "k_combine<2, float, 2, 4, 1, 0>" 20 gpurun_out/dispatch_series.json || exit 1
 fi
 if [[ $STAGE == all || $STAGE == kernels ]]; then
   run timeout -k 10 300 python tools/bench_kernels.py "$@" > gpurun_out/bench_kernels.jsonl 2> gpurun_out/bench_kernels.err || { tail -20 gpurun_out/bench_kernels.err; exit 1; }
@@ -42,6 +46,15 @@ fi
 if [[ $STAGE == all || $STAGE == host ]]; then
   run timeout -k 10 300 python tools/bench_host.py "$@" > gpurun_out/bench_host.jsonl 2> gpurun_out/bench_host.err || { tail -20 gpurun_out/bench_host.err; exit 1; }
   cat gpurun_out/bench_host.jsonl
+fi
+if [[ $STAGE == bench_ab ]]; then
+  # the driver's command with and without the prewarm, interleaved
+  for r in 1 2; do
+    for pw in 0 300; do
+      run timeout -k 10 400 python3 bench.py --gpus 1 --steps 20 --warmup 5 --prewarm-ms $pw --no-kernels > gpurun_out/bench_pw${pw}_$r.json 2>> gpurun_out/bench_ab.err || exit 1
+      cut -c1-400 gpurun_out/bench_pw${pw}_$r.json
+    done
+  done
 fi
 if [[ $STAGE == kernels_ab ]]; then
   # fixed-tree programs (default) against the generic masked program
