@@ -69,6 +69,9 @@ def parse():
                          "Infinity Cache: the number is HBM-bound, not cache-bound)")
     ap.add_argument("--exchange", default="auto", choices=["auto", "p2p", "pipe", "pipe2", "pipe8", "coll"])
     ap.add_argument("--tune-steps", type=int, default=5)
+    ap.add_argument("--variant-timeout", type=float, default=60.0,
+                    help="N > 1: seconds one checked step of an exchange variant may take before the "
+                         "variant counts as hung (its communicator is aborted and rebuilt)")
     ap.add_argument("--no-kernels", action="store_true",
                     help="N = 1: skip the C3 / C4 / C5 combine-kernel rates after the timed region")
     ap.add_argument("--transport", default="rccl", choices=["rccl", "host"],
@@ -371,12 +374,31 @@ def reference_run(cfg, world, n, dev, want_time):
     return digests, secs, reps
 
 
-def phase_breakdown(comm, step, coll, world, nbytes, reps=3):
+def plan_bytes(mvx, coll, world, rank, n, cnts, dtype, op):
+    """Bytes this rank sends and receives in phase A (exchange) and phase C
+    (distribution) of its plan (mvx_plan_build), for the per-link reading of
+    the phase rates: over direct xGMI links each peer's share travels on its
+    own link."""
+    kind = mvx.COLL_ALLREDUCE if coll == "allreduce" else mvx.COLL_REDUCE_SCATTER
+    P = mvx.plan(kind, world, rank, n, dtype, op, recvcnts=cnts if coll == "reduce_scatter" else None)
+    E = P.esize
+    out = {}
+    for ph, snd, rcv in (("A", P.a_send, P.a_recv), ("C", P.b_send, P.b_recv)):
+        s_peer = [snd[q].cnt * E for q in range(world) if q != rank]
+        r_peer = [rcv[q].cnt * E for q in range(world) if q != rank]
+        out[ph] = {"sent": sum(s_peer), "received": sum(r_peer),
+                   "max_per_peer": max(s_peer + r_peer) if world > 1 else 0,
+                   "peers": sum(1 for v in r_peer if v)}
+    return out
+
+
+def phase_breakdown(comm, step, coll, world, nbytes, pb, reps=3):
     """Untimed, after the timed region: `reps` more steps with HIP events
     around phase A (exchange), B (combine) and C (distribution) on the launch
     stream (mvx_comm_set_phase_timing); the median of each, MAX over ranks,
-    with the rate each phase reached: A / C as bytes each rank sends over
-    xGMI per ms, B as the combine's HBM bytes."""
+    with the rate each phase reached: A / C as the bytes each rank sends and
+    receives per ms (and per link: the largest single peer's share over the
+    phase time, against XGMI_LINK_GBS), B as the combine's HBM bytes."""
     import torch
     import torch.distributed as dist
     comm.set_phase_timing(True)
@@ -393,16 +415,42 @@ def phase_breakdown(comm, step, coll, world, nbytes, reps=3):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         out[key + "_ms"] = None if t.item() < 0 else round(float(t.item()), 4)
     p = world
-    wire = (p - 1) * nbytes / p          # bytes each rank sends in phase A (and C)
-    if out["A_ms"]:
-        out["A_GBs_per_rank"] = round(wire / (out["A_ms"] * 1e-3) / 1e9, 1)
+    for ph in ("A", "C"):
+        b = pb[ph]
+        out[ph + "_bytes"] = {"sent": b["sent"], "received": b["received"], "peers": b["peers"],
+                              "max_per_peer": b["max_per_peer"]}
+        ms = out[ph + "_ms"]
+        if ms and (b["sent"] or b["received"]):
+            sec = ms * 1e-3
+            out[ph + "_GBs_per_rank"] = {"sent": round(b["sent"] / sec / 1e9, 1),
+                                         "received": round(b["received"] / sec / 1e9, 1),
+                                         "per_link": round(b["max_per_peer"] / sec / 1e9, 1),
+                                         "link_frac": round(b["max_per_peer"] / sec / 1e9 / XGMI_LINK_GBS, 4)}
     if out["B_ms"]:
         out["B_hbm_GBs"] = round((p + 1) * nbytes / p / (out["B_ms"] * 1e-3) / 1e9, 1)
-    if out["C_ms"] and coll == "allreduce":
-        out["C_GBs_per_rank"] = round(wire / (out["C_ms"] * 1e-3) / 1e9, 1)
     out["note"] = ("one untimed step per sample with events between the phases; "
                    "the pipelined variant overlaps them (total only)")
     return out
+
+
+def _fail_injected(name, rank):
+    """MVX_BENCH_FAIL=variant@rank: that rank's steps under that exchange
+    variant report an error after running (a test of the variant choice)"""
+    spec = os.environ.get("MVX_BENCH_FAIL", "")
+    return any(x == "%s@%d" % (name, rank) for x in spec.split(",") if x)
+
+
+def _wait_stream(stream, seconds):
+    """True once the stream drained, False after `seconds` (a hung transfer)"""
+    t0 = time.perf_counter()
+    while not stream.query():
+        if time.perf_counter() - t0 > seconds:
+            return False
+        time.sleep(0.0005)
+    return True
+
+
+EXCH_NAMES = {-1: "none", 0: "p2p", 1: "pipe", 2: "coll"}
 
 
 def run_multi(args, mvx, dev, world, rank, local):
@@ -415,11 +463,14 @@ def run_multi(args, mvx, dev, world, rank, local):
     n -= n % world
     nbytes = n * E
     stream = torch.cuda.current_stream()
-    if args.transport == "host":
-        tp = importlib.import_module("mvapich-cce_amd.transport")
-        comm = mvx.Comm.from_transport(tp.TorchP2PTransport(), dev.index)
-    else:
-        comm = mvx.Comm.from_torch_distributed(dev.index)
+    tp = importlib.import_module("mvapich-cce_amd.transport") if args.transport == "host" else None
+
+    def new_comm():
+        if tp is not None:
+            return mvx.Comm.from_transport(tp.TorchP2PTransport(), dev.index)
+        return mvx.Comm.from_torch_distributed(dev.index)
+
+    comm = new_comm()
     sets = max(1, min(args.sets, 2))
     sendbuf = [synth(cfg, n, rank, dev) for _ in range(sets)]
     nrecv = n // world if coll == "reduce_scatter" else n
@@ -427,14 +478,18 @@ def run_multi(args, mvx, dev, world, rank, local):
     cnts = [n // world] * world
     comm.reserve(2 * nbytes)
     it = [0]
+    cur = {"name": None, "comm": comm}
 
     def step():
         s = it[0] % sets
         it[0] += 1
+        c = cur["comm"]
         if coll == "allreduce":
-            rc = comm.allreduce_async(sendbuf[s], recvbuf[s], n, dtype, op, stream)
+            rc = c.allreduce_async(sendbuf[s], recvbuf[s], n, dtype, op, stream)
         else:
-            rc = comm.reduce_scatter_async(sendbuf[s], recvbuf[s], cnts, dtype, op, stream)
+            rc = c.reduce_scatter_async(sendbuf[s], recvbuf[s], cnts, dtype, op, stream)
+        if rc == 0 and _fail_injected(cur["name"], rank):
+            rc = 15          # MPI_ERR_OTHER, after a complete step
         if rc:
             raise RuntimeError("%s rc=%d" % (coll, rc))
 
@@ -454,50 +509,101 @@ def run_multi(args, mvx, dev, world, rank, local):
         dist.broadcast_object_list(box, src=0)
         ref = box[0]
 
-    def check():
-        """one untimed step on set 0, every rank's digest against rank 0's reference"""
+    def agree(flag):
+        """every rank's status, MAX over ranks (gloo: the host side, which a
+        stuck GPU stream cannot block)"""
+        t = torch.tensor([flag], dtype=torch.int64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return int(t.item())
+
+    def trial():
+        """one untimed step of the current variant on set 0: 0 ok, 1 an
+        error return, 2 the step never completed"""
         it[0] = 0
-        step()
-        torch.cuda.synchronize()
+        try:
+            step()
+        except RuntimeError:
+            return 1
+        return 0 if _wait_stream(stream, args.variant_timeout) else 2
+
+    def parity_check():
+        """set 0's result on every rank against the reference's digests"""
+        if ref is None:
+            return None
         mine = _digest(recvbuf[0].cpu().numpy())
         allg = [None] * world
         dist.all_gather_object(allg, mine)
         return allg == ref
 
-    # exchange variants: timed, the fastest chosen on rank 0; each reports
-    # its parity against the reference
+    # exchange variants in EXCH order (p2p first, coll last): each gets one
+    # checked step, and is timed only if every rank completed it without an
+    # error; a variant that errs or never completes on any rank is recorded
+    # and left out of the choice (a hung one first tears the communicator
+    # down and builds a fresh one)
     names = list(EXCH) if args.exchange == "auto" else [args.exchange]
     tried = {}
     for name in names:
         mode, slices = EXCH[name]
-        comm.set_exchange(mode, slices)
-        if ref is not None:
-            ok = check()
-        else:
-            ok = None
-            step()      # untimed: RCCL sets up a variant's connections on its first use
+        cur["name"] = name
+        status = 1 if cur["comm"].set_exchange(mode, slices) else 0
+        if agree(status) == 0:
+            status = trial()
+        worst = agree(status)
+        ok, ran = None, None
+        if worst == 0:
+            ok = parity_check()
+            ran = EXCH_NAMES.get(cur["comm"].last_exchange(), "?")
+            if ran != EXCH_NAMES[mode]:
+                ran += " (fallback)"
+        entry = {"ran": ran}
+        if worst:
+            entry.update(ms_per_step=None, parity=None,
+                         error="an error return on some rank" if worst == 1 else
+                               "a step did not complete within %.0f s" % args.variant_timeout)
+            tried[name] = entry
+            if worst == 2:
+                cur["comm"].abort()
+                torch.cuda.synchronize()
+                cur["comm"] = new_comm()
+                cur["comm"].reserve(2 * nbytes)
+            continue
         t = torch.zeros(1, dtype=torch.float64)
         torch.cuda.synchronize()
         dist.barrier()
         t0 = time.perf_counter()
-        for _ in range(args.tune_steps):
-            step()
-        torch.cuda.synchronize()
+        try:
+            for _ in range(args.tune_steps):
+                step()
+            torch.cuda.synchronize()
+            terr = 0
+        except RuntimeError:
+            terr = 1
         t[0] = time.perf_counter() - t0
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        tried[name] = {"ms_per_step": round(float(t.item()) * 1e3 / args.tune_steps, 4), "parity": ok}
-    # the fastest variant whose parity did not fail (a MISMATCH stays on
-    # record in exchange_tuning but is never the one timed)
-    ok_names = [k for k in names if tried[k]["parity"] is not False] or names
+        if agree(terr):
+            entry.update(ms_per_step=None, parity=ok, error="an error return on some rank while tuning")
+        else:
+            entry.update(ms_per_step=round(float(t.item()) * 1e3 / args.tune_steps, 4), parity=ok)
+        tried[name] = entry
+    # the fastest variant that ran clean and whose parity did not fail (a
+    # MISMATCH stays on record in exchange_tuning but is never the one timed)
+    ok_names = [k for k in names if tried[k]["ms_per_step"] is not None and tried[k]["parity"] is not False]
+    if not ok_names:
+        if rank == 0:
+            sys.stderr.write("bench: no exchange variant ran clean with parity: %s\n" % json.dumps(tried))
+        return None
     choice = min(ok_names, key=lambda k: tried[k]["ms_per_step"])
     box = [choice]
     dist.broadcast_object_list(box, src=0)
     choice = box[0]
-    comm.set_exchange(*EXCH[choice])
+    cur["name"] = choice
+    cur["comm"].set_exchange(*EXCH[choice])
     parity = tried[choice]["parity"]
 
     times = timed(args, step, stream, world)
-    phases = phase_breakdown(comm, step, coll, world, nbytes)
+    ran = EXCH_NAMES.get(cur["comm"].last_exchange(), "?")
+    pb = plan_bytes(mvx, coll, world, rank, n, cnts, dtype, op)
+    phases = phase_breakdown(cur["comm"], step, coll, world, nbytes, pb)
     p = world
     sec = times["t_job"] / args.steps
     if coll == "allreduce":
@@ -516,11 +622,12 @@ def run_multi(args, mvx, dev, world, rank, local):
                  {"workload": "%s: %s %d MiB per rank, RCCL xGMI exchange + reference-order combine"
                               % (cfg, desc, nbytes // MIB),
                   "vector_bytes_per_rank": nbytes, "parallelism": "dp%d (blocks sharded over ranks)" % p,
-                  "exchange": choice, "exchange_tuning": tried, "transport": args.transport}, roof)
+                  "exchange": choice, "exchange_ran": ran, "exchange_tuning": tried,
+                  "transport": args.transport}, roof)
     out["parity"] = (("bit-exact vs the reference schedule, all %d ranks" % p) if parity
                      else ("MISMATCH" if parity is False else None))
     out["cpu_baseline"] = cpu
-    comm.free()
+    cur["comm"].free()
     return out
 
 
@@ -546,10 +653,12 @@ def main():
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     dist.init_process_group("gloo", rank=rank, world_size=world)
     out = run_multi(args, mvx, dev, world, rank, local)
-    if rank == 0:
+    if rank == 0 and out is not None:
         print(json.dumps(out), flush=True)
     dist.barrier()
     dist.destroy_process_group()
+    if out is None:
+        sys.exit(1)
 
 
 if __name__ == "__main__":

@@ -54,6 +54,14 @@ typedef struct mvx_transport {
     int (*send)(void *ctx, const void *buf, size_t bytes, int peer, void *stream);
     int (*recv)(void *ctx, void *buf, size_t bytes, int peer, void *stream);
     int (*end)(void *ctx, void *stream);
+    /* Optional (both or neither; NULL = MVX_EXCH_COLL runs as MVX_EXCH_P2P
+     * on this transport).  Same completion rules as a phase.
+     *   alltoall:  block j of sendbuf (`bytes` each) goes to rank j; rank j's
+     *              block for this rank lands in block j of recvbuf
+     *   allgather: in place -- this rank's block is at buf + rank * bytes;
+     *              on return block j holds rank j's block, for every j */
+    int (*alltoall)(void *ctx, const void *sendbuf, void *recvbuf, size_t bytes, void *stream);
+    int (*allgather)(void *ctx, void *buf, size_t bytes, void *stream);
 } mvx_transport;
 int mvx_comm_init_transport(MPI_Comm *comm, int rank, int size, int device,
                             const mvx_transport *transport);
@@ -84,6 +92,15 @@ int mvx_comm_reserve(MPI_Comm comm, size_t bytes);
 #define MVX_EXCH_COLL 2
 int mvx_comm_set_exchange(MPI_Comm comm, int mode, int slices);
 int mvx_comm_get_exchange(MPI_Comm comm, int *mode, int *slices);
+/* The variant the last collective call on `comm` actually ran: the one set,
+ * or MVX_EXCH_P2P where it falls back (COLL on an irregular plan, a user op,
+ * host buffers or a transport without collectives; PIPE on a plan too small
+ * to slice); -1 when the call moved nothing between ranks. */
+int mvx_comm_last_exchange(MPI_Comm comm, int *mode);
+/* Tear down a communicator without waiting for its outstanding transfers
+ * (ncclCommAbort): the way out of a transfer that never completes.  The
+ * handle is freed as by mvx_comm_free. */
+int mvx_comm_abort(MPI_Comm *comm);
 /* Per-phase timing (diagnostics): with timing on, each device-buffer call
  * records HIP events on its stream around phase A (exchange), B (combine)
  * and C (distribution).  mvx_comm_phase_times waits for the last timed call
@@ -174,7 +191,13 @@ int PMPI_Op_free(MPI_Op *);
 /* ---- stream-ordered variants (device buffers only) ---------------------
  * Calls on one communicator share its staging pool: issue them on one
  * stream (as MPI orders a communicator's collectives), or synchronise the
- * streams between calls. */
+ * streams between calls.
+ *
+ * Buffer kinds must agree across ranks within one call: every rank passes
+ * device buffers, or every rank passes host buffers.  Host-buffer calls
+ * move in slices (lengths fixed by count, p and the type, the same on every
+ * rank); device-buffer calls move whole blocks; a mix pairs transfers of
+ * different sizes. */
 int mvx_reduce_async(const void *sendbuf, void *recvbuf, int count,
                      MPI_Datatype datatype, MPI_Op op, int root, MPI_Comm comm,
                      void *hip_stream);

@@ -74,16 +74,32 @@ struct MPIR_COMMUNICATOR {                     /* mpid/ch2/comm.h:65-113 */
     int use_return_handler;
     int error_handler;
     int permanent;
+#ifdef _SMP_
+    void *mutex;                               /* mpid/ch_gen2/comm.h:121 (ch2: an empty
+                                                  MPID_THREAD_DS_LOCK_DECLARE, ch2/mpid.h:56) */
+#endif
     int msgform;
     void *adiCollCtx;
     MPIR_COLLOPS collops;
     struct MPIR_COMMUNICATOR *comm_next;
     char *comm_name;
-#ifdef _SMP_                                   /* mpid/ch_gen2/comm.h:162-181 */
+#ifdef _SMP_                                   /* mpid/ch_gen2/comm.h:139-181 (ch_smp, ch_psm and
+                                                  ch_hybrid declare the same members) */
+    struct Collbuf *collbuf;
+    unsigned int is_mcast_enabled, is_alltoall_enabled, is_barrier_enabled, is_allgather_enabled;
+    int rdma_barrier_id;
+    int togle;
     MPI_Comm leader_comm, shmem_comm, parent_comm;
     int parent;
     int *leader_map, *leader_rank;
     int shmem_comm_rank, shmem_coll_ok, leader_group_size;
+    int bcast_fd, bcast_index;
+    void *bcast_mmap_ptr;
+    char *bcast_shmem_file;
+    int bcast_seg_size, allg_cyclic_ok;
+    int new_group;                             /* MPI_Group */
+    MPI_Comm new_comm;
+    int *new_ranks;
 #endif
 };
 

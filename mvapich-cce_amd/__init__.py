@@ -136,10 +136,12 @@ def _load():
     c.mvx_copy.argtypes = [vp, vp, sz]
     c.mvx_stream_synchronize.argtypes = [vp]
     c.mvx_comm_free.argtypes = [pi]
+    c.mvx_comm_abort.argtypes = [pi]
     c.mvx_comm_set_stream.argtypes = [i, vp]
     c.mvx_comm_reserve.argtypes = [i, sz]
     c.mvx_comm_set_exchange.argtypes = [i, i, i]
     c.mvx_comm_get_exchange.argtypes = [i, pi, pi]
+    c.mvx_comm_last_exchange.argtypes = [i, pi]
     c.mvx_comm_set_phase_timing.argtypes = [i, i]
     c.mvx_comm_phase_times.argtypes = [i, ctypes.POINTER(ctypes.c_float)]
     c.MPI_Comm_size.argtypes = [i, pi]

@@ -157,6 +157,12 @@ class Comm:
         h = ctypes.c_int(self.handle)
         coll().mvx_comm_free(ctypes.byref(h))
 
+    def abort(self):
+        """mvx_comm_abort: tear down without waiting for outstanding
+        transfers (ncclCommAbort)."""
+        h = ctypes.c_int(self.handle)
+        return coll().mvx_comm_abort(ctypes.byref(h))
+
     def set_stream(self, stream=None):
         return coll().mvx_comm_set_stream(self.handle, stream_handle(stream))
 
@@ -173,6 +179,15 @@ class Comm:
         if rc:
             raise RuntimeError("mvx_comm_get_exchange rc=%d" % rc)
         return m.value, s.value
+
+    def last_exchange(self):
+        """The variant the last call ran (mvx_comm_last_exchange): EXCH_*,
+        or -1 when it moved nothing between ranks."""
+        m = ctypes.c_int()
+        rc = coll().mvx_comm_last_exchange(self.handle, ctypes.byref(m))
+        if rc:
+            raise RuntimeError("mvx_comm_last_exchange rc=%d" % rc)
+        return m.value
 
     def set_phase_timing(self, on=True):
         """Record HIP events around phases A / B / C of every device call

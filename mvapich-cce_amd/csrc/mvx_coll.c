@@ -81,6 +81,7 @@ typedef struct {
     int tev_ready, tev_kind;    /* events created; what the last timed call recorded (TEV_*) */
     hipEvent_t tev[4];          /* start, after A, after B, after C */
     int keep;                   /* this call's (op, type) is undefined: every combine keeps its inout */
+    int ran_exch;               /* the variant the last call ran (mvx_comm_last_exchange), -1 none */
 } mvx_comm_t;
 
 static mvx_comm_t g_comms[MAX_COMMS];
@@ -281,11 +282,14 @@ int mvx_stream_synchronize(void *stream)
     return hipStreamSynchronize((hipStream_t)stream) == hipSuccess ? MPI_SUCCESS : MPI_ERR_OTHER;
 }
 
-int mvx_comm_free(MPI_Comm *comm)
+static int comm_release(MPI_Comm *comm, int abort)
 {
     mvx_comm_t *c = comm ? get_comm(*comm) : NULL;
     if (!c) return ERR_COMM_NULL_CODE;
-    if (c->nccl) ncclCommDestroy(c->nccl);
+    if (c->nccl) {
+        if (abort) ncclCommAbort(c->nccl);
+        else ncclCommDestroy(c->nccl);
+    }
     if (c->pool) hipFree(c->pool);
     if (c->hpool) hipFree(c->hpool);
     if (c->upool) hipFree(c->upool);
@@ -306,6 +310,12 @@ int mvx_comm_free(MPI_Comm *comm)
     *comm = 0;
     return MPI_SUCCESS;
 }
+
+int mvx_comm_free(MPI_Comm *comm) { return comm_release(comm, 0); }
+
+/* ncclCommAbort stops the communicator's kernels without waiting for their
+ * peers; the staging memory is freed after it */
+int mvx_comm_abort(MPI_Comm *comm) { return comm_release(comm, 1); }
 
 int MPI_Comm_size(MPI_Comm comm, int *size)
 {
@@ -359,6 +369,15 @@ int mvx_comm_get_exchange(MPI_Comm comm, int *mode, int *slices)
     if (!c) return ERR_COMM_NULL_CODE;
     if (mode) *mode = c->exch;
     if (slices) *slices = c->exch_slices;
+    return MPI_SUCCESS;
+}
+
+int mvx_comm_last_exchange(MPI_Comm comm, int *mode)
+{
+    mvx_comm_t *c = get_comm(comm);
+    if (!c) return ERR_COMM_NULL_CODE;
+    if (!mode) return MPI_ERR_ARG;
+    *mode = c->ran_exch;
     return MPI_SUCCESS;
 }
 
@@ -976,6 +995,9 @@ typedef struct mvx_xport {
     int (*end)(struct mvx_xport *);
     int (*send)(struct mvx_xport *, const void *, size_t, int, hipStream_t);
     int (*recv)(struct mvx_xport *, void *, size_t, int, hipStream_t);
+    /* whole-communicator exchanges of the COLL variant (NULL: none) */
+    int (*alltoall)(struct mvx_xport *, const void *, void *, size_t, hipStream_t);
+    int (*allgather)(struct mvx_xport *, void *, size_t, hipStream_t);
     ncclComm_t nccl;
     loopback_t *lb;
     const mvx_transport *ops;   /* caller-supplied transport */
@@ -990,6 +1012,11 @@ static int nc_send(mvx_xport *t, const void *b, size_t n, int peer, hipStream_t 
 { return ncclSend(b, n, ncclUint8, peer, t->nccl, st) == ncclSuccess ? 0 : MPI_ERR_OTHER; }
 static int nc_recv(mvx_xport *t, void *b, size_t n, int peer, hipStream_t st)
 { return ncclRecv(b, n, ncclUint8, peer, t->nccl, st) == ncclSuccess ? 0 : MPI_ERR_OTHER; }
+static int nc_alltoall(mvx_xport *t, const void *s, void *r, size_t n, hipStream_t st)
+{ return ncclAllToAll(s, r, n, ncclUint8, t->nccl, st) == ncclSuccess ? 0 : MPI_ERR_OTHER; }
+/* in place: the send operand is this rank's block of the receive buffer */
+static int nc_allgather(mvx_xport *t, void *b, size_t n, hipStream_t st)
+{ return ncclAllGather((char *)b + (size_t)t->me * n, b, n, ncclUint8, t->nccl, st) == ncclSuccess ? 0 : MPI_ERR_OTHER; }
 
 /* a caller-supplied transport; nested start / end pairs form one group */
 static int op_start(mvx_xport *t)
@@ -1006,6 +1033,10 @@ static int op_send(mvx_xport *t, const void *b, size_t n, int peer, hipStream_t 
 { return t->ops->send(t->ops->ctx, b, n, peer, (void *)st) ? MPI_ERR_OTHER : 0; }
 static int op_recv(mvx_xport *t, void *b, size_t n, int peer, hipStream_t st)
 { return t->ops->recv(t->ops->ctx, b, n, peer, (void *)st) ? MPI_ERR_OTHER : 0; }
+static int op_alltoall(mvx_xport *t, const void *s, void *r, size_t n, hipStream_t st)
+{ return t->ops->alltoall(t->ops->ctx, s, r, n, (void *)st) ? MPI_ERR_OTHER : 0; }
+static int op_allgather(mvx_xport *t, void *b, size_t n, hipStream_t st)
+{ return t->ops->allgather(t->ops->ctx, b, n, (void *)st) ? MPI_ERR_OTHER : 0; }
 
 static int lb_nop(mvx_xport *t) { (void)t; return 0; }
 static int lb_send(mvx_xport *t, const void *b, size_t n, int peer, hipStream_t st)
@@ -1346,6 +1377,7 @@ static int run_device_pipe(mvx_comm_t *c, const job_t *J, hipStream_t st)
     nsl = (span + cs - 1) / cs;
     if (nsl <= 1) return run_device_plain(c, J, st);
     if ((rc = pipe_streams(c))) return rc;
+    c->ran_exch = MVX_EXCH_PIPE;
     for (r = 0; r < J->nr; r++) {
         plan_slice(&J->P[r], 0, cs, &g_pipe[0][r]);
         X0[r].sendbuf = J->send[r];
@@ -1419,6 +1451,7 @@ static int coll_regular(const mvx_plan *P, long *blk)
 static int run_device_coll(mvx_comm_t *c, const job_t *J, long b, hipStream_t st)
 {
     const mvx_plan *P = &J->P[0];
+    mvx_xport *t = &J->t[0];
     const size_t bb = (size_t)(b * P->esize);
     const char *leafp[MVX_MAXP];
     rank_exec_t X;
@@ -1430,17 +1463,16 @@ static int run_device_coll(mvx_comm_t *c, const job_t *J, long b, hipStream_t st
     X.wide_n = wide_temps(P);
     X.wide_slot = al256(bb + SLOT_STAGGER);
     if ((rc = grow(&c->pool, &c->pool_bytes, stage + X.wide_slot * (size_t)X.wide_n))) return rc;
+    c->ran_exch = MVX_EXCH_COLL;
     if ((rc = tev(c, 0, st))) return rc;
-    if (ncclAllToAll(J->send[0], c->pool, bb, ncclUint8, c->nccl, st) != ncclSuccess) return MPI_ERR_OTHER;
+    if ((rc = t->alltoall(t, J->send[0], c->pool, bb, st))) return rc;
     if ((rc = tev(c, 1, st))) return rc;
     for (s = 0; s < P->p; s++)
         leafp[s] = s == P->rank ? J->send[0] + (size_t)P->rank * bb : c->pool + (size_t)s * bb;
     S.base = c->pool + stage; S.slot = X.wide_slot; S.used = 0; S.cap = X.wide_n;
     if ((rc = combine(c, P, leafp, J->recv[0] + P->c_dst_off * P->esize, &S, st))) return rc;
     if ((rc = tev(c, 2, st))) return rc;
-    if (P->coll == MVX_COLL_ALLREDUCE &&
-        ncclAllGather(J->recv[0] + (size_t)P->rank * bb, J->recv[0], bb, ncclUint8, c->nccl, st) != ncclSuccess)
-        return MPI_ERR_OTHER;
+    if (P->coll == MVX_COLL_ALLREDUCE && (rc = t->allgather(t, J->recv[0], bb, st))) return rc;
     if ((rc = tev(c, 3, st))) return rc;
     if (c->timing) c->tev_kind = TEV_PHASES;
     return MPI_SUCCESS;
@@ -1450,9 +1482,10 @@ static int run_device_coll(mvx_comm_t *c, const job_t *J, long b, hipStream_t st
 static int run_device(mvx_comm_t *c, const job_t *J, hipStream_t st)
 {
     long blk;
+    c->ran_exch = MVX_EXCH_P2P;   /* unless a variant below takes the call */
     if (c->exch == MVX_EXCH_PIPE) return run_device_pipe(c, J, st);
-    if (c->exch == MVX_EXCH_COLL && J->nr == 1 && J->t[0].nccl && J->P[0].opkind == MVX_OPKIND_PREDEFINED &&
-        coll_regular(&J->P[0], &blk))
+    if (c->exch == MVX_EXCH_COLL && J->nr == 1 && J->t[0].alltoall && J->t[0].allgather &&
+        J->P[0].opkind == MVX_OPKIND_PREDEFINED && coll_regular(&J->P[0], &blk))
         return run_device_coll(c, J, blk, st);
     return run_device_plain(c, J, st);
 }
@@ -1632,14 +1665,21 @@ static int run_staged(mvx_comm_t *c, const job_t *J, hipStream_t st)
         X[r].sendbuf = S.dsend[r];
         X[r].recvbuf = S.drecv[r];
     }
-    /* slice length: every local rank's pieces of one slice fill one bounce
-     * slot of STAGE_SLICE_BYTES per local rank (a virtual communicator's
-     * ranks each bring their own vectors: without the factor its pieces
-     * shrink to ~1 MiB and per-copy overheads dominate); a multiple of 256
-     * elements keeps each operand's alignment */
+    /* slice length, a multiple of 256 elements (keeps each operand's
+     * alignment).  One rank per process: STAGE_SLICE_BYTES spread over p
+     * pieces (a rank's plan reads at most p ranges of its sendbuf -- p - 1
+     * blocks out plus its own -- and writes at most p of its recvbuf).  That
+     * depends only on p and the type, never on this rank's plan, so every
+     * rank of a call slices alike and its transfers pair up.  A virtual
+     * communicator (all ranks in this process, sliced together) fills one
+     * slot of STAGE_SLICE_BYTES per local rank with all its ranks' pieces:
+     * without the nr factor its pieces shrink to ~1 MiB and per-copy
+     * overheads dominate.  The bounce slots hold this process's pieces. */
+    c->ran_exch = MVX_EXCH_P2P;
     {
         const long E = J->P[0].esize;
-        long cs = STAGE_SLICE_BYTES * J->nr / (E * (pieces > 0 ? pieces : 1));
+        long cs = J->nr > 1 ? STAGE_SLICE_BYTES * J->nr / (E * (pieces > 0 ? pieces : 1))
+                            : STAGE_SLICE_BYTES / (E * J->P[0].p);
         cs &= ~255L;
         if (cs < 256) cs = 256;
         S.cs = cs;
@@ -1847,6 +1887,7 @@ static int run(mvx_comm_t *c, const call_t *k, hipStream_t st, int blocking)
     int e, ts;
 
     if (c->local) return MPI_ERR_COMM;   /* virtual comms use *_multi */
+    c->ran_exch = -1;
     mvx_dtype_info(k->dt, &e, &ts);
     rc = mvx_plan_build_tuned(&P, k->coll, c->size, c->rank, k->count, k->recvcnts,
                               k->dt, k->op, k->root, op_kind(k->op), &c->tune);
@@ -1875,9 +1916,11 @@ static int run(mvx_comm_t *c, const call_t *k, hipStream_t st, int blocking)
     memset(&t, 0, sizeof t);
     if (c->has_ops) {
         t.start = op_start; t.end = op_end; t.send = op_send; t.recv = op_recv;
+        if (c->ops.alltoall && c->ops.allgather) { t.alltoall = op_alltoall; t.allgather = op_allgather; }
         t.ops = &c->ops; t.st = st;
     } else {
         t.start = nc_start; t.end = nc_end; t.send = nc_send; t.recv = nc_recv;
+        t.alltoall = nc_alltoall; t.allgather = nc_allgather;
         t.nccl = c->nccl;
     }
     t.me = c->rank;

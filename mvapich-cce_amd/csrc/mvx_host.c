@@ -56,6 +56,11 @@ int mvx_host_pinned(const void *p)
 #define PC_MAX_WORKERS 31
 #define PC_MIN_SPLIT (1L << 20)    /* below this one thread copies */
 
+/* one split copy at a time: `job` is held from publishing a copy until its
+ * last part is done, so callers on several threads (MPIR_* op functions,
+ * two communicators) queue whole jobs and no worker skips a generation */
+static pthread_mutex_t g_pc_job = PTHREAD_MUTEX_INITIALIZER;
+
 static struct {
     pthread_mutex_t mu;
     pthread_cond_t go, done;
@@ -135,6 +140,9 @@ void mvx_pcopy(void *dst, const void *src, size_t bytes)
         memcpy(dst, src, bytes);
         return;
     }
+    pthread_mutex_unlock(&g_pc.mu);
+    pthread_mutex_lock(&g_pc_job);
+    pthread_mutex_lock(&g_pc.mu);
     g_pc.dst = (char *)dst; g_pc.src = (const char *)src; g_pc.bytes = bytes;
     g_pc.pending = n;
     g_pc.gen++;
@@ -144,6 +152,7 @@ void mvx_pcopy(void *dst, const void *src, size_t bytes)
     pthread_mutex_lock(&g_pc.mu);
     while (g_pc.pending) pthread_cond_wait(&g_pc.done, &g_pc.mu);
     pthread_mutex_unlock(&g_pc.mu);
+    pthread_mutex_unlock(&g_pc_job);
 }
 
 int mvx_copy_threads(void)

@@ -42,7 +42,7 @@ def main():
         comm = mvx.Comm.from_transport(tp.TorchP2PTransport(), dev)
     else:
         comm = mvx.Comm.from_torch_distributed(dev)
-    report = {"rank": rank, "checked": 0, "fails": []}
+    report = {"rank": rank, "checked": 0, "fails": [], "ran": {}}
 
     def inputs(dtype, tot, fill):
         if fill is None:
@@ -86,6 +86,10 @@ def main():
         else:
             rref = O.reduce_scatter(s8, r8, cnts, dtype, op)
         report["checked"] += 1
+        # which exchange variant the call actually ran (mvx_comm_last_exchange)
+        ran = report["ran"].setdefault(tag.split()[0] if tag else "-", {})
+        key = str(comm.last_exchange())
+        ran[key] = ran.get(key, 0) + 1
         ok = rc == rref[rank]
         # a 329 rank's recvbuf too: an undefined pair moves the data as the
         # reference's algorithm does
@@ -98,9 +102,7 @@ def main():
         if not ok:
             report["fails"].append([coll, dtype, op, tot, where, root, rc, rref[rank], tag])
 
-    modes = [("p2p", mvx.EXCH_P2P, 0), ("pipe", mvx.EXCH_PIPE, 3)]
-    if transport == "rccl":
-        modes.append(("coll", mvx.EXCH_COLL, 0))
+    modes = [("p2p", mvx.EXCH_P2P, 0), ("pipe", mvx.EXCH_PIPE, 3), ("coll", mvx.EXCH_COLL, 0)]
     if suite == "small":
         cases = [(102, 10), (100, 10), (111, 17), (105, 8), (110, 18), (103, 6)]
         for name, mode, sl in modes:
@@ -113,6 +115,10 @@ def main():
                         check("red", dtype, op, n, where, root=world - 1, tag=name)
                     for base in (3, 40000, 140000):
                         check("rs", dtype, op, [base + (q % 2) for q in range(world)], where, tag=name)
+                        # equal blocks: the plans the COLL variant takes whole
+                        check("rs", dtype, op, [base] * world, where, tag=name)
+                    # a multiple of p above the Rabenseifner threshold (p = 4)
+                    check("ar", dtype, op, 4096 * world * 4, where, tag=name)
                     check("scan", dtype, op, 5000, where, tag=name)
     elif suite == "random":
         # the same seeded case sequence on every rank (tests/test_gpu_fuzz.py's

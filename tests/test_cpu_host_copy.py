@@ -52,3 +52,32 @@ print("ok")
     p = subprocess.run([sys.executable, "-c", code, lib, str(min(threads, ncpu))], env=env,
                        capture_output=True, text=True, timeout=120)
     assert p.returncode == 0 and "ok" in p.stdout, p.stderr[-2000:]
+
+
+def test_pcopy_concurrent_callers(mvx):
+    """Several threads copying at once (ctypes drops the GIL around each
+    call): every job completes whole -- callers queue behind one another
+    instead of overwriting the pool's one job record."""
+    import threading
+    lib = mvx.coll()
+    lib.mvx_pcopy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
+    lib.mvx_pcopy.restype = None
+    bad = []
+
+    def worker(t):
+        rng = np.random.default_rng(100 + t)
+        for i in range(30):
+            nb = int(rng.integers(1 << 20, 6 << 20))
+            s = rng.integers(0, 256, nb, dtype=np.uint8)
+            d = np.zeros(nb, np.uint8)
+            lib.mvx_pcopy(d.ctypes.data, s.ctypes.data, nb)
+            if not np.array_equal(d, s):
+                bad.append((t, i, nb))
+
+    ts = [threading.Thread(target=worker, args=(t,)) for t in range(4)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(120)
+    assert not any(t.is_alive() for t in ts)
+    assert not bad, bad[:5]

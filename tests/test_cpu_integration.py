@@ -236,3 +236,28 @@ def test_host_buffers_take_mvapich_path(mvx, oracle, shim, monkeypatch):
 def test_smp_build_loads(mvx):
     lib = _lib(smp=True)
     assert lib.h_host_calls() == 0
+
+
+def test_check_headers_match_reference_layout():
+    """The compile-check headers lay out every member the shim reads at the
+    offsets the reference's own headers give (plain ch_shmem and the _SMP_
+    devices' ch_gen2 communicator), and the committed ref_layout.h -- which
+    layout_assert.c holds the check build to with _Static_assert -- is what
+    those headers give today (integration/check/ref_layout.py)."""
+    if not os.path.isdir(REF):
+        pytest.skip("reference tree not present")
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        "ref_layout", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                   "integration", "check", "ref_layout.py"))
+    rl = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(rl)
+    lay = rl.reference_layouts(REF)
+    assert rl.check_layouts(False) == lay["plain"]
+    assert rl.check_layouts(True) == lay["smp"]
+    names = dict(lay["smp"])
+    # the _SMP_ communicator carries ch_gen2's mutex pointer and RDMA
+    # collective members before the shmem fields the shim reads
+    assert int(names["comm_t.collops"]) > int(dict(lay["plain"])["comm_t.collops"])
+    with open(os.path.join(os.path.dirname(rl.__file__), "ref_layout.h")) as f:
+        assert f.read() == rl.header_text(lay)

@@ -64,11 +64,23 @@ def _launch(world, transport, suite, timeout):
 
 @pytest.mark.parametrize("world", [2, 3, 4])
 def test_executor_across_processes_host_transport(world):
-    reports = _launch(world, "host", "small", 240)
+    """Every exchange variant, COLL included: over the host transport its
+    all-to-all / in-place all-gather run as the transport's alltoall /
+    allgather hooks (gloo), with the staging layout, leaf pointers and
+    gather offsets of the RCCL path."""
+    reports = _launch(world, "host", "small", 300)
     for rep in reports:
         assert rep["checked"] > 100
         assert not rep["fails"], rep["fails"][:5]
         assert not rep["transport_errors"], rep["transport_errors"][:3]
+        ran = rep["ran"]
+        # the COLL variant ran whole on the regular plans (p equal blocks);
+        # every other call under it reports the P2P fallback, never COLL
+        assert ran["coll"].get("2", 0) > 0, ran
+        assert ran["p2p"].get("2", 0) == 0 and ran["pipe"].get("2", 0) == 0, ran
+        assert ran["p2p"].get("1", 0) == 0, ran
+        if world > 1:
+            assert ran["pipe"].get("1", 0) > 0, ran
 
 
 @pytest.mark.parametrize("world", [2, 3])
@@ -93,25 +105,72 @@ def test_rccl_multirank(world):
             assert not rep["fails"], rep["fails"][:5]
 
 
+def _bench_host(cfg, extra_env=None, world=2):
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    env.update(extra_env or {})
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", str(world), "--steps", "3", "--warmup", "1", "--tune-steps", "1", "--mib", "32",
+           "--config", cfg, "--transport", "host"]
+    p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    return p
+
+
 @pytest.mark.parametrize("cfg", ["c3", "c4", "c5"])
 def test_bench_multi_gpu_leg_host_transport(cfg):
     """The N > 1 bench leg under torchrun (2 ranks on one GPU, host
     transport): one JSON line with parity bit-exact for every exchange
-    variant tried, and a 2-thread CPU baseline."""
-    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"),
-           "--gpus", "2", "--steps", "3", "--warmup", "1", "--tune-steps", "1", "--mib", "32",
-           "--config", cfg, "--transport", "host"]
-    p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    variant tried -- each one reporting the variant that actually ran (COLL
+    over the transport's alltoall / allgather hooks) -- a 2-thread CPU
+    baseline, and every per-phase field the 8-GPU run prints."""
+    p = _bench_host(cfg)
     assert p.returncode == 0, p.stderr[-3000:]
     line = [x for x in p.stdout.splitlines() if x.startswith("{")]
     assert len(line) == 1, p.stdout[-2000:]
     d = json.loads(line[0])
     assert d["n_gpus"] == 2 and d["value"] > 0
     assert d["parity"].startswith("bit-exact"), d
-    assert all(v["parity"] for v in d["config"]["exchange_tuning"].values()), d["config"]["exchange_tuning"]
+    tuning = d["config"]["exchange_tuning"]
+    assert all(v["parity"] for v in tuning.values()), tuning
+    assert tuning["p2p"]["ran"] == "p2p" and tuning["coll"]["ran"] == "coll", tuning
+    assert tuning["pipe"]["ran"] == "pipe", tuning
+    assert d["config"]["exchange_ran"] == tuning[d["config"]["exchange"]]["ran"]
     assert d["cpu_baseline"]["cores"] == 2
     assert d["config"]["transport"] == "host"
     ph = d["roofline"]["phases"]
     assert ph["total_ms"] > 0, ph
+    S = d["config"]["vector_bytes_per_rank"]
+    assert ph["A_bytes"]["received"] == ph["A_bytes"]["sent"] == S // 2, ph
+    assert ph["A_bytes"]["peers"] == 1 and ph["A_bytes"]["max_per_peer"] == S // 2
+    if cfg == "c4":
+        assert ph["C_bytes"]["received"] == 0
+    else:
+        assert ph["C_bytes"]["received"] == S // 2
+    if d["config"]["exchange"] != "pipe" and not d["config"]["exchange"].startswith("pipe"):
+        assert set(ph["A_GBs_per_rank"]) == {"sent", "received", "per_link", "link_frac"}, ph
+
+
+@pytest.mark.parametrize("bad", ["coll@1", "p2p@0,pipe8@1"])
+def test_bench_survives_a_failing_variant(bad):
+    """A variant that returns an error on one rank (MVX_BENCH_FAIL) is
+    recorded and left out; the line still comes, from the other variants,
+    with parity bit-exact."""
+    p = _bench_host("c3", {"MVX_BENCH_FAIL": bad})
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = [x for x in p.stdout.splitlines() if x.startswith("{")]
+    assert len(line) == 1, p.stdout[-2000:]
+    d = json.loads(line[0])
+    tuning = d["config"]["exchange_tuning"]
+    failed = [x.split("@")[0] for x in bad.split(",")]
+    for v in failed:
+        assert tuning[v]["ms_per_step"] is None and "error" in tuning[v], tuning
+    assert d["config"]["exchange"] not in failed
+    assert d["parity"].startswith("bit-exact"), d
+
+
+def test_bench_no_clean_variant_exits_nonzero():
+    """Every variant failing: no throughput line, a nonzero exit."""
+    p = _bench_host("c3", {"MVX_BENCH_FAIL": ",".join("%s@1" % v for v in
+                                                      ("p2p", "pipe", "pipe2", "pipe8", "coll"))})
+    assert p.returncode != 0
+    assert not [x for x in p.stdout.splitlines() if x.startswith("{")]
