@@ -73,7 +73,9 @@ template <typename B> struct pp;
 // the x87 types: every op is dozens of integer instructions, so their
 // combines are ALU-bound and keep full occupancy (no body kernels, no
 // residency cap: the 8-leaf x87 SUM tree ran 109.7 us at 2 blocks per CU
-// against 74.4 us uncapped, profiles/r02/bench_kernels_x87.jsonl)
+// against 74.4 us uncapped, profiles/r02/bench_kernels_x87.jsonl; an
+// uncapped body kernel with the short argument block ran the MAXLOC tree at
+// 114 us against 108-112 us through k_combine, profiles/r03/bench_kernels_x87_ab.jsonl)
 template <typename T> struct alu_heavy { static constexpr bool v = false; };
 template <> struct alu_heavy<xf80> { static constexpr bool v = true; };
 template <> struct alu_heavy<pxi> { static constexpr bool v = true; };

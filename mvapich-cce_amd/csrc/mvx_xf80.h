@@ -49,16 +49,16 @@ typedef unsigned __int128 u128;
 
 enum { K_ZERO = 0, K_FIN, K_INF, K_QNAN, K_SNAN, K_BAD };
 
+// written as selects: on the device every lane classifies its own operand,
+// and nested ifs became exec-mask branches around each class
 XF_FN int klass(uint64_t m, uint32_t e)
 {
     const bool j = (m >> 63) != 0;
-    if (e == 0x7fff) {
-        if (!j) return K_BAD;                       // pseudo-infinity / pseudo-NaN
-        if ((m << 1) == 0) return K_INF;
-        return (m >> 62) & 1 ? K_QNAN : K_SNAN;
-    }
-    if (e == 0) return m == 0 ? K_ZERO : K_FIN;     // denormal or pseudo-denormal
-    return j ? K_FIN : K_BAD;                       // unnormal
+    const int top = !j ? K_BAD                      // pseudo-infinity / pseudo-NaN
+                  : (m << 1) == 0 ? K_INF : ((m >> 62) & 1 ? K_QNAN : K_SNAN);
+    const int bottom = m == 0 ? K_ZERO : K_FIN;     // denormal or pseudo-denormal
+    const int mid = j ? K_FIN : K_BAD;              // unnormal
+    return e == 0x7fff ? top : (e == 0 ? bottom : mid);
 }
 
 XF_FN xf80 with_bits(xf80 pads, uint64_t m, uint32_t se)
@@ -273,19 +273,27 @@ XF_FN xf80 mul(xf80 a, xf80 b)
     return round_pack(a, s, e, P);
 }
 
-// x87 compare: -1, 0, 1, or 2 = unordered (NaN or invalid encoding)
+// x87 compare: -1, 0, 1, or 2 = unordered (NaN or invalid encoding).
+// Branch-free: unordered is every class from K_QNAN up (exponent 0x7fff
+// except an infinity, or an unnormal); magnitudes order by (exponent, with
+// denormals and pseudo-denormals at 1; significand), zero below all; one
+// sign flip.  The MPI_MAX / MIN / MAXLOC / MINLOC trees run one of these per
+// step, and the branchy form left more scalar exec-mask work than vector work
+// in their loop (tools: --save-temps of mvx_ops_loc.hip).
 XF_FN int cmp(const xf80 &a, const xf80 &b)
 {
     const uint32_t ea = a.se & 0x7fff, eb = b.se & 0x7fff;
-    const int ka = klass(a.m, ea), kb = klass(b.m, eb);
-    if (ka >= K_QNAN || kb >= K_QNAN) return 2;
-    if (ka == K_ZERO && kb == K_ZERO) return 0;
+    const bool ja = (a.m >> 63) != 0, jb = (b.m >> 63) != 0;
+    const bool ua = ea == 0x7fff ? !(ja && (a.m << 1) == 0) : (ea != 0 && !ja);
+    const bool ub = eb == 0x7fff ? !(jb && (b.m << 1) == 0) : (eb != 0 && !jb);
+    const bool za = ea == 0 && a.m == 0, zb = eb == 0 && b.m == 0;
+    const uint32_t xa = za ? 0u : (ea ? ea : 1u), xb = zb ? 0u : (eb ? eb : 1u);
+    const bool gt = xa > xb || (xa == xb && a.m > b.m);
+    const bool eq = xa == xb && a.m == b.m;
     const uint32_t sa = a.se >> 15, sb = b.se >> 15;
-    if (sa != sb) return sa ? -1 : 1;
-    const u128 A = ka == K_ZERO ? 0 : ((u128)(ea ? ea : 1) << 64) | a.m;
-    const u128 B = kb == K_ZERO ? 0 : ((u128)(eb ? eb : 1) << 64) | b.m;
-    const int c = A == B ? 0 : (A < B ? -1 : 1);
-    return sa ? -c : c;
+    const int c = eq ? 0 : (gt != (sa != 0) ? 1 : -1);      // magnitude order, sign applied
+    const int r = (za && zb) ? 0 : (sa != sb ? (sa ? -1 : 1) : c);
+    return (ua || ub) ? 2 : r;
 }
 
 XF_FN bool truth(const xf80 &a)                       // `a != 0`, unordered is true
@@ -323,13 +331,12 @@ template <bool MIN>
 XF_FN pxi loc(pxi a, pxi b)
 {
     const int c = cmp(a.v, b.v);
+    const bool take = c == (MIN ? 1 : -1);
+    const int32_t lmin = a.l < b.l ? a.l : b.l;
     pxi r = a;
-    if (c == 0) {
-        r.l = a.l < b.l ? a.l : b.l;
-    } else if (c == (MIN ? 1 : -1)) {
-        r.v = with_bits(a.v, b.v.m, b.v.se);
-        r.l = b.l;
-    }
+    r.v.m = take ? b.v.m : a.v.m;
+    r.v.se = take ? b.v.se : a.v.se;
+    r.l = c == 0 ? lmin : (take ? b.l : a.l);
     return r;
 }
 

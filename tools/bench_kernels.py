@@ -111,6 +111,8 @@ def main():
         run(mvx, "X2-max", mvx.MPI_MAX, mvx.MPI_LONG_DOUBLE, 2, 1, 256 * MIB, 4)
         run(mvx, "X3-sum", mvx.MPI_SUM, mvx.MPI_LONG_DOUBLE, 8, 0, 32 * MIB, 4)
         run(mvx, "X5-maxloc", mvx.MPI_MAXLOC, mvx.MPI_LONG_DOUBLE_INT, 8, 0, 64 * MIB, 2)
+        run(mvx, "X5-minloc", mvx.MPI_MINLOC, mvx.MPI_LONG_DOUBLE_INT, 8, 0, 64 * MIB, 2)
+        run(mvx, "X3-max", mvx.MPI_MAX, mvx.MPI_LONG_DOUBLE, 8, 0, 32 * MIB, 4)
 
 
 if __name__ == "__main__":
