@@ -69,6 +69,8 @@ def parse():
                          "Infinity Cache: the number is HBM-bound, not cache-bound)")
     ap.add_argument("--exchange", default="auto", choices=["auto", "p2p", "pipe", "pipe2", "pipe8", "coll"])
     ap.add_argument("--tune-steps", type=int, default=5)
+    ap.add_argument("--gloo-timeout", type=float, default=600.0,
+                    help="N > 1: seconds any gloo operation may wait for a peer")
     ap.add_argument("--variant-timeout", type=float, default=60.0,
                     help="N > 1: seconds one checked step of an exchange variant may take before the "
                          "variant counts as hung (its communicator is aborted and rebuilt)")
@@ -651,7 +653,13 @@ def main():
         run_single(args, mvx, dev)
         return
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # gloo bootstraps, agrees and checks (and is the host transport's byte
+    # mover): a peer that never arrives fails the call after this long
+    # instead of gloo's 30 minutes; rank 0's reference run (tens of seconds
+    # at C5 x 8) stays well inside it
+    import datetime
+    dist.init_process_group("gloo", rank=rank, world_size=world,
+                            timeout=datetime.timedelta(seconds=args.gloo_timeout))
     out = run_multi(args, mvx, dev, world, rank, local)
     if rank == 0 and out is not None:
         print(json.dumps(out), flush=True)

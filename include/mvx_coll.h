@@ -99,7 +99,8 @@ int mvx_comm_get_exchange(MPI_Comm comm, int *mode, int *slices);
 int mvx_comm_last_exchange(MPI_Comm comm, int *mode);
 /* Tear down a communicator without waiting for its outstanding transfers
  * (ncclCommAbort): the way out of a transfer that never completes.  The
- * handle is freed as by mvx_comm_free. */
+ * handle is freed as by mvx_comm_free; the staging memory is not (work
+ * queued behind the aborted transfers may still read it). */
 int mvx_comm_abort(MPI_Comm *comm);
 /* Per-phase timing (diagnostics): with timing on, each device-buffer call
  * records HIP events on its stream around phase A (exchange), B (combine)

@@ -290,11 +290,16 @@ static int comm_release(MPI_Comm *comm, int abort)
         if (abort) ncclCommAbort(c->nccl);
         else ncclCommDestroy(c->nccl);
     }
-    if (c->pool) hipFree(c->pool);
-    if (c->hpool) hipFree(c->hpool);
-    if (c->upool) hipFree(c->upool);
-    if (c->uhost) hipHostFree(c->uhost);
-    if (c->xpool) hipFree(c->xpool);
+    /* an aborted communicator's staging may still be read by work queued
+     * behind the aborted transfers (a combine waiting on its stream): those
+     * allocations are left to the process rather than freed under it */
+    if (!abort) {
+        if (c->pool) hipFree(c->pool);
+        if (c->hpool) hipFree(c->hpool);
+        if (c->upool) hipFree(c->upool);
+        if (c->uhost) hipHostFree(c->uhost);
+        if (c->xpool) hipFree(c->xpool);
+    }
     if (c->cstream) {
         int i;
         hipStreamDestroy(c->cstream);
@@ -314,7 +319,7 @@ static int comm_release(MPI_Comm *comm, int abort)
 int mvx_comm_free(MPI_Comm *comm) { return comm_release(comm, 0); }
 
 /* ncclCommAbort stops the communicator's kernels without waiting for their
- * peers; the staging memory is freed after it */
+ * peers; the staging memory is not freed (see comm_release) */
 int mvx_comm_abort(MPI_Comm *comm) { return comm_release(comm, 1); }
 
 int MPI_Comm_size(MPI_Comm comm, int *size)
@@ -1877,6 +1882,15 @@ static int undefined_moves(const mvx_comm_t *c, int coll)
     return !(c->tune.smp && (coll == MVX_COLL_ALLREDUCE || coll == MVX_COLL_REDUCE));
 }
 
+/* 1 if rank's plan sends or receives anything */
+static int plan_moves(const mvx_plan *P)
+{
+    int s;
+    for (s = 0; s < P->p; s++)
+        if (P->a_send[s].cnt || P->a_recv[s].cnt || P->b_send[s].cnt || P->b_recv[s].cnt) return 1;
+    return 0;
+}
+
 static int run(mvx_comm_t *c, const call_t *k, hipStream_t st, int blocking)
 {
     static mvx_plan P;
@@ -1935,6 +1949,7 @@ static int run(mvx_comm_t *c, const call_t *k, hipStream_t st, int blocking)
     c->keep = keep;
     rc = run_job(c, &J, st, blocking);
     c->keep = 0;
+    if (!plan_moves(&P)) c->ran_exch = -1;   /* nothing crossed between ranks */
     return rc ? rc : vrc;
 }
 

@@ -207,6 +207,22 @@ def test_rccl_single_rank_world(mvx, oracle):
     assert comm.allreduce_async(da, db, n, 10, 102) == 0
     torch.cuda.synchronize()
     assert np.array_equal(db.cpu().numpy(), a)
+    # the variant each call ran: p = 1 moves nothing between ranks
+    assert comm.last_exchange() == -1
+    comm.free()
+    # mvx_comm_abort (ncclCommAbort) with a call still queued: the handle is
+    # released at once and the queued work completes; a fresh communicator
+    # on the same group works
+    comm = mvx.Comm.from_torch_distributed(0)
+    db.zero_()
+    assert comm.allreduce_async(da, db, n, 10, 102) == 0
+    assert comm.abort() == 0
+    torch.cuda.synchronize()
+    assert np.array_equal(db.cpu().numpy(), a)
+    comm = mvx.Comm.from_torch_distributed(0)
+    db.zero_()
+    assert mvx.MPI_Allreduce(da, db, n, 10, 102, comm) == 0
+    assert np.array_equal(db.cpu().numpy(), a)
     comm.free()
 
 
