@@ -455,6 +455,15 @@ def _wait_stream(stream, seconds):
 EXCH_NAMES = {-1: "none", 0: "p2p", 1: "pipe", 2: "coll"}
 
 
+def choose_variant(names, tried):
+    """The fastest variant that ran clean (timed) and whose parity did not
+    fail, in `names` order on ties; None when there is none.  A MISMATCH
+    stays on record in exchange_tuning but is never the one timed."""
+    ok = [k for k in names if tried.get(k, {}).get("ms_per_step") is not None
+          and tried[k].get("parity") is not False]
+    return min(ok, key=lambda k: tried[k]["ms_per_step"]) if ok else None
+
+
 def run_multi(args, mvx, dev, world, rank, local):
     import torch
     import torch.distributed as dist
@@ -573,13 +582,13 @@ def run_multi(args, mvx, dev, world, rank, local):
         torch.cuda.synchronize()
         dist.barrier()
         t0 = time.perf_counter()
-        try:
-            for _ in range(args.tune_steps):
+        terr = 0
+        for _ in range(args.tune_steps):      # every rank issues every step
+            try:
                 step()
-            torch.cuda.synchronize()
-            terr = 0
-        except RuntimeError:
-            terr = 1
+            except RuntimeError:
+                terr = 1
+        torch.cuda.synchronize()
         t[0] = time.perf_counter() - t0
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         if agree(terr):
@@ -589,12 +598,11 @@ def run_multi(args, mvx, dev, world, rank, local):
         tried[name] = entry
     # the fastest variant that ran clean and whose parity did not fail (a
     # MISMATCH stays on record in exchange_tuning but is never the one timed)
-    ok_names = [k for k in names if tried[k]["ms_per_step"] is not None and tried[k]["parity"] is not False]
-    if not ok_names:
+    choice = choose_variant(names, tried)
+    if choice is None:
         if rank == 0:
             sys.stderr.write("bench: no exchange variant ran clean with parity: %s\n" % json.dumps(tried))
         return None
-    choice = min(ok_names, key=lambda k: tried[k]["ms_per_step"])
     box = [choice]
     dist.broadcast_object_list(box, src=0)
     choice = box[0]
