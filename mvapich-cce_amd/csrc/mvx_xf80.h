@@ -126,62 +126,55 @@ XF_FN xf80 round_pack(xf80 pads, uint32_t s, int e, u128 S)
 // and encoding as add()'s general path (whose 128-bit shifts dominate the
 // emulated add on the device), which handles everything else.  Returns false
 // when the operands are outside that case.
+//
+// Written as selects: the same-sign sum and the opposite-sign difference
+// (with its normalisation) are both computed and one is kept, and the
+// rounding carry and the overflow are selects too.  Lanes of a wave disagree
+// on the sign case about half the time on mixed-sign data, so a branch ran
+// both sides anyway, plus the exec-mask bookkeeping around each.
 XF_FN bool add_normal(xf80 a, xf80 b, xf80 *out)
 {
     const uint32_t ea = a.se & 0x7fff, eb = b.se & 0x7fff;
-    if (ea - 1u >= 0x7ffeu || eb - 1u >= 0x7ffeu || !(a.m >> 63) || !(b.m >> 63)) return false;
-    uint32_t sa = a.se >> 15, sb = b.se >> 15;
-    int xa = (int)ea, xb = (int)eb;
-    uint64_t ma = a.m, mb = b.m;
-    if (xb > xa || (xb == xa && mb > ma)) {          // |a| >= |b| from here
-        const int t = xa; xa = xb; xb = t;
-        const uint64_t tm = ma; ma = mb; mb = tm;
-        const uint32_t ts = sa; sa = sb; sb = ts;
-    }
+    const bool normal = ea - 1u < 0x7ffeu && eb - 1u < 0x7ffeu && (a.m >> 63) && (b.m >> 63);
+    // |a| >= |b| from here
+    const bool swap = eb > ea || (eb == ea && b.m > a.m);
+    const int xa = (int)(swap ? eb : ea), xb = (int)(swap ? ea : eb);
+    const uint64_t ma = swap ? b.m : a.m, mb = swap ? a.m : b.m;
+    const uint32_t sa = (swap ? b.se : a.se) >> 15, sb = (swap ? a.se : b.se) >> 15;
     const int d = xa - xb;
-    if (d > 64) return false;
+    if (!normal || d > 64) return false;
     // B = mb * 2^(64 - d) as hi:lo below A = ma:0 (no bit is lost for d <= 64)
-    const uint64_t hi = d == 64 ? 0 : mb >> d;
-    const uint64_t lo = d == 0 ? 0 : (d == 64 ? mb : mb << (64 - d));
-    uint64_t rh, rl;
-    int e = xa;
-    if (sa == sb) {
-        rh = ma + hi;
-        rl = lo;
-        if (rh < ma) {                                // carry out: shift right, keep sticky
-            rl = (rh << 63) | (rl >> 1) | (rl & 1);
-            rh = (rh >> 1) | (1ull << 63);
-            ++e;
-        }
-    } else {
-        rl = 0 - lo;
-        rh = ma - hi - (lo != 0);
-        if (rh == 0 && rl == 0) {                     // exact cancellation: +0
-            *out = with_bits(a, 0, 0);
-            return true;
-        }
-        int lz = rh ? __builtin_clzll(rh) : 64 + __builtin_clzll(rl);
-        if (lz > e - 1) lz = e - 1;                   // a tiny result stays denormal
-        if (lz >= 64) {
-            rh = rl << (lz - 64);
-            rl = 0;
-        } else if (lz > 0) {
-            rh = (rh << lz) | (rl >> (64 - lz));
-            rl <<= lz;
-        }
-        e -= lz;
-    }
-    if ((rl >> 63) && ((rl << 1) || (rh & 1))) {      // round to nearest even
-        if (++rh == 0) {
-            rh = 1ull << 63;
-            ++e;
-        }
-    }
-    if (e >= 0x7fff) {
-        *out = with_bits(a, 1ull << 63, (sa << 15) | 0x7fff);   // overflow
-        return true;
-    }
-    *out = with_bits(a, rh, (sa << 15) | ((rh >> 63) ? (uint32_t)e : 0u));
+    const uint64_t hi = d >= 64 ? 0 : mb >> (d & 63);
+    const uint64_t lo = d == 0 ? 0 : (d >= 64 ? mb : mb << ((64 - d) & 63));
+    // same signs: the sum, shifted right with a sticky bit on a carry out
+    const uint64_t sh = ma + hi;
+    const bool carry = sh < ma;
+    const uint64_t add_h = carry ? ((sh >> 1) | (1ull << 63)) : sh;
+    const uint64_t add_l = carry ? ((sh << 63) | (lo >> 1) | (lo & 1)) : lo;
+    const int add_e = xa + (carry ? 1 : 0);
+    // opposite signs: the difference, normalised (a tiny result stays denormal)
+    const uint64_t dl = 0 - lo;
+    const uint64_t dh = ma - hi - (lo != 0 ? 1 : 0);
+    const bool cancel = dh == 0 && dl == 0;                  // exact cancellation: +0
+    int lz = dh ? __builtin_clzll(dh) : 64 + __builtin_clzll(dl | 1);
+    if (lz > xa - 1) lz = xa - 1;
+    const uint64_t sub_h = lz >= 64 ? dl << ((lz - 64) & 63)
+                         : (lz > 0 ? (dh << (lz & 63)) | (dl >> ((64 - lz) & 63)) : dh);
+    const uint64_t sub_l = lz >= 64 ? 0 : (lz > 0 ? dl << (lz & 63) : dl);
+    const int sub_e = xa - lz;
+    const bool same = sa == sb;
+    const uint64_t rh = same ? add_h : sub_h, rl = same ? add_l : sub_l;
+    const int e = same ? add_e : sub_e;
+    // round to nearest even; a carry out of the significand bumps the exponent
+    const bool up = (rl >> 63) && ((rl << 1) || (rh & 1));
+    const uint64_t r1 = rh + (up ? 1 : 0);
+    const bool wrap = up && r1 == 0;
+    const uint64_t r = wrap ? (1ull << 63) : r1;
+    const int e2 = e + (wrap ? 1 : 0);
+    const bool over = e2 >= 0x7fff;                          // overflow: infinity
+    const uint64_t m = over ? (1ull << 63) : r;
+    const uint32_t enc = over ? 0x7fffu : ((r >> 63) ? (uint32_t)e2 : 0u);
+    *out = (!same && cancel) ? with_bits(a, 0, 0) : with_bits(a, m, (sa << 15) | enc);
     return true;
 }
 
