@@ -546,13 +546,59 @@ def run_multi(args, mvx, dev, world, rank, local):
         dist.all_gather_object(allg, mine)
         return allg == ref
 
-    # exchange variants in EXCH order (p2p first, coll last): each gets one
-    # checked step, and is timed only if every rank completed it without an
-    # error; a variant that errs or never completes on any rank is recorded
-    # and left out of the choice (a hung one first tears the communicator
-    # down and builds a fresh one)
+    def measure(name):
+        """the K timed steps (and the per-phase breakdown) of variant `name`:
+        one candidate line"""
+        cur["name"] = name
+        cur["comm"].set_exchange(*EXCH[name])
+        times = timed(args, step, stream, world)
+        ran = EXCH_NAMES.get(cur["comm"].last_exchange(), "?")
+        pb = plan_bytes(mvx, coll, world, rank, n, cnts, dtype, op)
+        phases = phase_breakdown(cur["comm"], step, coll, world, nbytes, pb)
+        p = world
+        sec = times["t_job"] / args.steps
+        if coll == "allreduce":
+            busbw = 2 * (p - 1) / p * nbytes / sec / 1e9
+            note = "busbw = 2(p-1)/p*S/t"
+        else:
+            busbw = (p - 1) / p * nbytes / sec / 1e9
+            note = "busbw = (p-1)/p*S/t"
+        links = min(p - 1, 7)
+        peak = links * XGMI_LINK_GBS
+        roof = {"bound": "xgmi", "achieved": round(busbw, 1), "peak": peak, "unit": "GB/s",
+                "frac": round(busbw / peak, 4), "traffic": None, "kernel": mvx.last_kernel(),
+                "note": "%s against %d direct xGMI links x %.0f GB/s" % (note, links, XGMI_LINK_GBS),
+                "combine_hbm_bytes_per_step": (p + 1) * nbytes // p, "phases": phases}
+        out = result(args, world, nbytes, times, {"c3": "f32", "c4": "int64", "c5": "f32+int32"}[cfg],
+                     {"workload": "%s: %s %d MiB per rank, RCCL xGMI exchange + reference-order combine"
+                                  % (cfg, desc, nbytes // MIB),
+                      "vector_bytes_per_rank": nbytes, "parallelism": "dp%d (blocks sharded over ranks)" % p,
+                      "exchange": name, "exchange_ran": ran, "exchange_tuning": None,
+                      "transport": args.transport}, roof)
+        parity = tried[name]["parity"]
+        out["parity"] = (("bit-exact vs the reference schedule, all %d ranks" % p) if parity
+                         else ("MISMATCH" if parity is False else None))
+        out["cpu_baseline"] = cpu
+        return out
+
+    # Exchange variants in EXCH order (p2p first, coll last).  Each gets one
+    # checked step, then --tune-steps timed steps if every rank completed it
+    # without an error; a variant that errs or never completes on any rank is
+    # recorded and left out (a hung one first tears the communicator down and
+    # builds a fresh one).  The first clean variant is measured for the line
+    # at once (K timed steps), and a later one is measured again only if its
+    # tuning steps ran faster -- so a line exists before any riskier variant
+    # runs, and a variant that wedges the GPU for good ends the run with the
+    # line already measured rather than with none.
     names = list(EXCH) if args.exchange == "auto" else [args.exchange]
     tried = {}
+    best = None
+
+    def finish(out):
+        if out is not None:
+            out["config"]["exchange_tuning"] = tried
+        return out
+
     for name in names:
         mode, slices = EXCH[name]
         cur["name"] = name
@@ -574,7 +620,13 @@ def run_multi(args, mvx, dev, world, rank, local):
             tried[name] = entry
             if worst == 2:
                 cur["comm"].abort()
-                torch.cuda.synchronize()
+                if agree(0 if _wait_stream(stream, args.variant_timeout) else 1):
+                    # still wedged after the abort: report what was measured
+                    entry["error"] += "; the stream stayed blocked after ncclCommAbort"
+                    if rank == 0 and best is not None:
+                        print(json.dumps(finish(best)), flush=True)
+                    sys.stdout.flush()
+                    os._exit(0 if best is not None else 1)
                 cur["comm"] = new_comm()
                 cur["comm"].reserve(2 * nbytes)
             continue
@@ -596,47 +648,21 @@ def run_multi(args, mvx, dev, world, rank, local):
         else:
             entry.update(ms_per_step=round(float(t.item()) * 1e3 / args.tune_steps, 4), parity=ok)
         tried[name] = entry
-    # the fastest variant that ran clean and whose parity did not fail (a
-    # MISMATCH stays on record in exchange_tuning but is never the one timed)
-    choice = choose_variant(names, tried)
-    if choice is None:
+        # measure for the line: the first clean variant, then any that tuned
+        # faster than the one measured (every rank decides alike: the tuning
+        # time is the MAX over ranks and parity is compared on every rank)
+        if choose_variant([name], tried) == name and (
+                best is None or entry["ms_per_step"] < tried[best["config"]["exchange"]]["ms_per_step"]):
+            box = [name]
+            dist.broadcast_object_list(box, src=0)
+            cand = measure(box[0])
+            if best is None or cand["ms_per_step"] < best["ms_per_step"]:
+                best = cand
+    if best is None:
         if rank == 0:
             sys.stderr.write("bench: no exchange variant ran clean with parity: %s\n" % json.dumps(tried))
         return None
-    box = [choice]
-    dist.broadcast_object_list(box, src=0)
-    choice = box[0]
-    cur["name"] = choice
-    cur["comm"].set_exchange(*EXCH[choice])
-    parity = tried[choice]["parity"]
-
-    times = timed(args, step, stream, world)
-    ran = EXCH_NAMES.get(cur["comm"].last_exchange(), "?")
-    pb = plan_bytes(mvx, coll, world, rank, n, cnts, dtype, op)
-    phases = phase_breakdown(cur["comm"], step, coll, world, nbytes, pb)
-    p = world
-    sec = times["t_job"] / args.steps
-    if coll == "allreduce":
-        busbw = 2 * (p - 1) / p * nbytes / sec / 1e9
-        note = "busbw = 2(p-1)/p*S/t"
-    else:
-        busbw = (p - 1) / p * nbytes / sec / 1e9
-        note = "busbw = (p-1)/p*S/t"
-    links = min(p - 1, 7)
-    peak = links * XGMI_LINK_GBS
-    roof = {"bound": "xgmi", "achieved": round(busbw, 1), "peak": peak, "unit": "GB/s",
-            "frac": round(busbw / peak, 4), "traffic": None, "kernel": mvx.last_kernel(),
-            "note": "%s against %d direct xGMI links x %.0f GB/s" % (note, links, XGMI_LINK_GBS),
-            "combine_hbm_bytes_per_step": (p + 1) * nbytes // p, "phases": phases}
-    out = result(args, world, nbytes, times, {"c3": "f32", "c4": "int64", "c5": "f32+int32"}[cfg],
-                 {"workload": "%s: %s %d MiB per rank, RCCL xGMI exchange + reference-order combine"
-                              % (cfg, desc, nbytes // MIB),
-                  "vector_bytes_per_rank": nbytes, "parallelism": "dp%d (blocks sharded over ranks)" % p,
-                  "exchange": choice, "exchange_ran": ran, "exchange_tuning": tried,
-                  "transport": args.transport}, roof)
-    out["parity"] = (("bit-exact vs the reference schedule, all %d ranks" % p) if parity
-                     else ("MISMATCH" if parity is False else None))
-    out["cpu_baseline"] = cpu
+    out = finish(best)
     cur["comm"].free()
     return out
 
