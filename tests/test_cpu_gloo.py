@@ -147,3 +147,33 @@ def test_plans_over_gloo(tmp_path, world):
     for r in range(world):
         txt = (tmp_path / ("rank%d.txt" % r)).read_text()
         assert txt == "", txt
+
+
+def _peer_worker(rank, world, port, out_dir):
+    sys.path[:0] = [ROOT, HERE]
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+    tp = importlib.import_module("mvapich-cce_amd.transport")
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    g = dist.new_group([1, 2])
+    got = []
+    if rank in (1, 2):
+        t = tp.TorchP2PTransport(group=g)
+        got = [t._peer(0), t._peer(1)]
+    assert tp.TorchP2PTransport()._peer(2) == 2
+    dist.barrier()
+    dist.destroy_process_group()
+    with open(os.path.join(out_dir, "peer%d.txt" % rank), "w") as f:
+        f.write(repr(got))
+
+
+def test_transport_maps_group_ranks_to_global(tmp_path):
+    """libmvx passes communicator ranks to the transport; with a sub-group,
+    TorchP2PTransport sends to and receives from the matching global ranks
+    (torch.distributed's dst / src are global even when a group is given)."""
+    import torch.multiprocessing as mp
+    mp.spawn(_peer_worker, args=(3, _free_port(), str(tmp_path)), nprocs=3, join=True)
+    assert (tmp_path / "peer0.txt").read_text() == "[]"
+    assert (tmp_path / "peer1.txt").read_text() == "[1, 2]"
+    assert (tmp_path / "peer2.txt").read_text() == "[1, 2]"
