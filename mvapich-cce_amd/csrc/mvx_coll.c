@@ -1670,8 +1670,7 @@ static int run_staged(mvx_comm_t *c, const job_t *J, hipStream_t st)
         X[r].sendbuf = S.dsend[r];
         X[r].recvbuf = S.drecv[r];
     }
-    /* slice length, a multiple of 256 elements (keeps each operand's
-     * alignment).  One rank per process: STAGE_SLICE_BYTES spread over p
+    /* slice length.  One rank per process: STAGE_SLICE_BYTES spread over p
      * pieces (a rank's plan reads at most p ranges of its sendbuf -- p - 1
      * blocks out plus its own -- and writes at most p of its recvbuf).  That
      * depends only on p and the type, never on this rank's plan, so every
@@ -1683,10 +1682,18 @@ static int run_staged(mvx_comm_t *c, const job_t *J, hipStream_t st)
     c->ran_exch = MVX_EXCH_P2P;
     {
         const long E = J->P[0].esize;
+        /* slices start at multiples of 256 bytes of every vector (each
+         * operand keeps its alignment): cs a multiple of m elements; for a
+         * large packed element m is 1 and a slice may hold a single element,
+         * where a fixed 256-element floor would size the bounce slots at
+         * 256 elements of it */
+        long g = E, h = 256, m;
+        while (h) { const long t = g % h; g = h; h = t; }      /* gcd(E, 256) */
+        m = 256 / g;
         long cs = J->nr > 1 ? STAGE_SLICE_BYTES * J->nr / (E * (pieces > 0 ? pieces : 1))
                             : STAGE_SLICE_BYTES / (E * J->P[0].p);
-        cs &= ~255L;
-        if (cs < 256) cs = 256;
+        cs -= cs % m;
+        if (cs < m) cs = m;
         S.cs = cs;
         bounce = (size_t)pieces * al256((size_t)(cs * E));
         if (bounce < 4096) bounce = 4096;
