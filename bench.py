@@ -69,6 +69,9 @@ def parse():
                          "Infinity Cache: the number is HBM-bound, not cache-bound)")
     ap.add_argument("--exchange", default="auto", choices=["auto", "p2p", "pipe", "pipe2", "pipe8", "coll"])
     ap.add_argument("--tune-steps", type=int, default=5)
+    ap.add_argument("--extra-configs", default="auto",
+                    help="N > 1: more BASELINE configs measured after the line, on the same communicator "
+                         "(auto: c4 at N = 4, c5 at N = 8; none; or a comma list)")
     ap.add_argument("--gloo-timeout", type=float, default=600.0,
                     help="N > 1: seconds any gloo operation may wait for a peer")
     ap.add_argument("--variant-timeout", type=float, default=60.0,
@@ -464,6 +467,76 @@ def choose_variant(names, tried):
     return min(ok, key=lambda k: tried[k]["ms_per_step"]) if ok else None
 
 
+# BASELINE's multi-GPU configs by GPU count: at N = 4 and N = 8 the line
+# also carries the config quoted at that count (after the timed region)
+EXTRA_AT = {4: ["c4"], 8: ["c5"]}
+
+
+def run_extra(args, mvx, dev, world, rank, comm, exch_name, cfg, agree, stream):
+    """After the line is measured: one more BASELINE config on the same
+    communicator -- its reference digests (rank 0, the reference schedule on
+    p host threads, untimed), one checked step (a hang or an error is
+    recorded, not fatal), then W + K timed steps.  Returns a summary dict."""
+    import torch
+    import torch.distributed as dist
+    coll, dtype, op, E, mib, desc = CONFIGS[cfg]
+    nbytes = (args.mib or mib) * MIB
+    n = nbytes // E
+    n -= n % world
+    nbytes = n * E
+    ref = None
+    if not args.no_cpu_baseline:
+        box = [reference_run(cfg, world, n, dev, False)[0] if rank == 0 else None]
+        dist.broadcast_object_list(box, src=0)
+        ref = box[0]
+    sendbuf = synth(cfg, n, rank, dev)
+    nrecv = n // world if coll == "reduce_scatter" else n
+    recvbuf = torch.empty(nrecv * E, dtype=torch.uint8, device=dev)
+    cnts = [n // world] * world
+    comm.reserve(2 * nbytes)
+    mode, slices = EXCH[exch_name]
+    comm.set_exchange(mode, slices)
+    out = {"config": cfg, "workload": "%s %d MiB per rank" % (desc, nbytes // MIB),
+           "vector_bytes_per_rank": nbytes, "exchange": exch_name}
+
+    def step():
+        if coll == "allreduce":
+            rc = comm.allreduce_async(sendbuf, recvbuf, n, dtype, op, stream)
+        else:
+            rc = comm.reduce_scatter_async(sendbuf, recvbuf, cnts, dtype, op, stream)
+        if rc:
+            raise RuntimeError("%s rc=%d" % (coll, rc))
+
+    try:
+        step()
+        status = 0 if _wait_stream(stream, args.variant_timeout) else 2
+    except RuntimeError:
+        status = 1
+    worst = agree(status)
+    if worst:
+        out["error"] = "an error return on some rank" if worst == 1 else "the checked step did not complete"
+        return out, worst
+    parity = None
+    if ref is not None:
+        allg = [None] * world
+        dist.all_gather_object(allg, _digest(recvbuf.cpu().numpy()))
+        parity = allg == ref
+    out["exchange_ran"] = EXCH_NAMES.get(comm.last_exchange(), "?")
+    times = timed(args, step, stream, world)
+    p = world
+    sec = times["t_job"] / args.steps
+    busbw = (2 if coll == "allreduce" else 1) * (p - 1) / p * nbytes / sec / 1e9
+    peak = min(p - 1, 7) * XGMI_LINK_GBS
+    out.update(value=round(world * nbytes * args.steps / times["t_job"] / GIB, 2), unit="GiB/s",
+               ms_per_step=round(sec * 1e3, 5), busbw_GBs=round(busbw, 1), frac=round(busbw / peak, 4),
+               xgmi_peak_GBs=peak,
+               parity=("bit-exact vs the reference schedule, all %d ranks" % p) if parity
+               else ("MISMATCH" if parity is False else None))
+    del sendbuf, recvbuf
+    torch.cuda.empty_cache()
+    return out, 0
+
+
 def run_multi(args, mvx, dev, world, rank, local):
     import torch
     import torch.distributed as dist
@@ -663,7 +736,25 @@ def run_multi(args, mvx, dev, world, rank, local):
             sys.stderr.write("bench: no exchange variant ran clean with parity: %s\n" % json.dumps(tried))
         return None
     out = finish(best)
-    cur["comm"].free()
+    # the other BASELINE configs quoted at this GPU count, on the same
+    # communicator and exchange variant, after the line's timed region
+    extras = EXTRA_AT.get(world, []) if args.extra_configs == "auto" else \
+        [c for c in args.extra_configs.split(",") if c and c != "none"]
+    others, aborted = [], False
+    for cfg2 in extras:
+        if cfg2 == cfg:
+            continue
+        res, worst = run_extra(args, mvx, dev, world, rank, cur["comm"], out["config"]["exchange"], cfg2,
+                               agree, stream)
+        others.append(res)
+        if worst == 2:           # a hang: leave the communicator, keep the line
+            cur["comm"].abort()
+            aborted = True
+            break
+    if others:
+        out["other_configs"] = others
+    if not aborted:
+        cur["comm"].free()
     return out
 
 

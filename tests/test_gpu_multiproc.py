@@ -178,3 +178,24 @@ def test_bench_no_clean_variant_exits_nonzero():
                                                       ("p2p", "pipe", "pipe2", "pipe8", "coll"))})
     assert p.returncode != 0
     assert not [x for x in p.stdout.splitlines() if x.startswith("{")]
+
+
+def test_bench_line_carries_the_other_baseline_configs():
+    """At N = 4 the line also carries C4 (Reduce_scatter BAND int64) measured
+    after the timed region on the same communicator: its own parity against
+    the reference schedule, time and bus bandwidth (host transport, 4 ranks
+    on one GPU, small vectors)."""
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", "4", "--steps", "2", "--warmup", "1", "--tune-steps", "1", "--mib", "16",
+           "--transport", "host"]
+    p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=400)
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = [x for x in p.stdout.splitlines() if x.startswith("{")]
+    assert len(line) == 1, p.stdout[-2000:]
+    d = json.loads(line[0])
+    assert d["config"]["workload"].startswith("c3") and d["parity"].startswith("bit-exact")
+    (o,) = d["other_configs"]
+    assert o["config"] == "c4" and o["parity"].startswith("bit-exact"), o
+    assert o["value"] > 0 and o["busbw_GBs"] > 0 and o["exchange"] == d["config"]["exchange"]
