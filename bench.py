@@ -79,9 +79,11 @@ def parse():
                          "variant counts as hung (its communicator is aborted and rebuilt)")
     ap.add_argument("--no-kernels", action="store_true",
                     help="N = 1: skip the C3 / C4 / C5 combine-kernel rates after the timed region")
-    ap.add_argument("--transport", default="rccl", choices=["rccl", "host"],
-                    help="host: ranks may share a GPU, bytes move through gloo (a test of the "
-                         "multi-GPU leg on a 1-GPU box; not a performance configuration)")
+    ap.add_argument("--transport", default="rccl", choices=["rccl", "host", "rccl-net"],
+                    help="host: ranks may share a GPU, bytes move through gloo; rccl-net: ranks may "
+                         "share a GPU, bytes move through RCCL's own socket transport (each rank "
+                         "names itself a separate host).  Both test the multi-GPU leg on a 1-GPU "
+                         "box; neither is a performance configuration")
     return ap.parse_args()
 
 
@@ -766,7 +768,9 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dev_index = local % torch.cuda.device_count() if args.transport == "host" else local
+    if args.transport == "rccl-net":
+        importlib.import_module("mvapich-cce_amd.transport").rccl_net_env(rank)
+    dev_index = local % torch.cuda.device_count() if args.transport != "rccl" else local
     torch.cuda.set_device(dev_index)
     dev = torch.device("cuda", dev_index)
     mvx = importlib.import_module("mvapich-cce_amd")

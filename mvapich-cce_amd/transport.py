@@ -26,6 +26,27 @@ _A2A = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c
 _AG = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p)
 
 
+def rccl_net_env(rank, env=None):
+    """Make RCCL itself carry the bytes between ranks that share one GPU.
+
+    RCCL's duplicate-GPU check compares (host hash, PCI bus id) of every
+    pair of ranks; the host hash is NCCL_HOSTID when that is set.  Giving
+    each rank its own host id makes them separate one-GPU "nodes", so RCCL
+    accepts the communicator and moves every byte through its network
+    transport (sockets over loopback, host-staged by its proxy thread):
+    the RCCL calls of the executor (grouped ncclSend / ncclRecv,
+    ncclAllToAll, in-place ncclAllGather, ncclCommAbort) run for real at
+    p > 1 on a one-GPU box.  Not a performance configuration -- on a node
+    every rank has its own GPU and RCCL picks xGMI P2P.  Must run before
+    the process's first RCCL call.  Returns the environment it changed."""
+    import os
+    env = os.environ if env is None else env
+    env["NCCL_HOSTID"] = "mvx-rank-%d" % rank
+    env.setdefault("NCCL_SOCKET_IFNAME", "lo")
+    env.setdefault("NCCL_IB_DISABLE", "1")
+    return env
+
+
 class Transport(ctypes.Structure):
     """Mirror of ``mvx_transport``."""
     _fields_ = [("ctx", ctypes.c_void_p), ("start", _START), ("send", _XFER), ("recv", _XFER), ("end", _END),

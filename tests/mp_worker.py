@@ -7,7 +7,10 @@ the collectives through its libmvx.so communicator and compares its own
 result with the oracle's replay of the reference schedule
 (oracle/coll_sim.c) computed over all ranks' inputs.  Writes a JSON report.
 
-  mp_worker.py RANK WORLD PORT OUT.json TRANSPORT(host|rccl) SUITE(small|full)
+  mp_worker.py RANK WORLD PORT OUT.json TRANSPORT(host|rccl|rccl-net) SUITE(small|random|full)
+
+rccl-net: RCCL communicators whose ranks may share one GPU, the bytes moved
+by RCCL's own socket transport (transport.rccl_net_env).
 """
 import json
 import os
@@ -32,10 +35,12 @@ def main():
     from oracle import oracle as O
     mvx = importlib.import_module("mvapich-cce_amd")
     from importlib import import_module
-    tp = import_module("mvapich-cce_amd.transport")
 
+    tp = import_module("mvapich-cce_amd.transport")
+    if transport == "rccl-net":
+        tp.rccl_net_env(rank)
     ndev = torch.cuda.device_count()
-    dev = rank % ndev if transport == "host" else rank
+    dev = rank % ndev if transport != "rccl" else rank
     torch.cuda.set_device(dev)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     if transport == "host":

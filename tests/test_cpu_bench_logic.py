@@ -45,3 +45,14 @@ def test_plan_bytes_match_the_partition():
     # MAXLOC at p = 2 is recursive doubling: the whole vector each way, no phase C
     b = bench.plan_bytes(mvx, "allreduce", 2, 0, n, None, bench.MPI_FLOAT_INT, bench.MPI_MAXLOC)
     assert b["A"]["sent"] == n * 8 and b["C"]["sent"] == 0
+
+
+def test_rccl_net_env_gives_each_rank_its_own_host():
+    """--transport rccl-net: distinct NCCL_HOSTID per rank (RCCL's
+    duplicate-GPU check keys on host hash + bus id), loopback sockets, and a
+    caller's own interface choice left alone."""
+    tp = importlib.import_module("mvapich-cce_amd.transport")
+    envs = [tp.rccl_net_env(r, {}) for r in range(8)]
+    assert len({e["NCCL_HOSTID"] for e in envs}) == 8
+    assert all(e["NCCL_SOCKET_IFNAME"] == "lo" and e["NCCL_IB_DISABLE"] == "1" for e in envs)
+    assert tp.rccl_net_env(3, {"NCCL_SOCKET_IFNAME": "eth0"})["NCCL_SOCKET_IFNAME"] == "eth0"

@@ -105,13 +105,31 @@ def test_rccl_multirank(world):
             assert not rep["fails"], rep["fails"][:5]
 
 
-def _bench_host(cfg, extra_env=None, world=2):
+@pytest.mark.parametrize("world", [2, 4])
+def test_rccl_multirank_net_transport(world):
+    """The RCCL executor itself at p > 1 on one GPU: each rank names itself
+    a separate host (NCCL_HOSTID, transport.rccl_net_env), so RCCL accepts
+    ranks that share the GPU and moves every byte through its socket
+    transport -- the grouped ncclSend / ncclRecv of P2P and PIPE and the
+    ncclAllToAll / in-place ncclAllGather of COLL, bit-exact against the
+    oracle's replay."""
+    for suite in ("small", "random"):
+        for rep in _launch(world, "rccl-net", suite, 600):
+            assert rep["checked"] > 0
+            assert not rep["fails"], rep["fails"][:5]
+            if suite == "small":
+                ran = rep["ran"]
+                assert ran["coll"].get("2", 0) > 0, ran
+                assert ran["pipe"].get("1", 0) > 0, ran
+
+
+def _bench_host(cfg, extra_env=None, world=2, transport="host"):
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
     env.update(extra_env or {})
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"),
            "--gpus", str(world), "--steps", "3", "--warmup", "1", "--tune-steps", "1", "--mib", "32",
-           "--config", cfg, "--transport", "host"]
+           "--config", cfg, "--transport", transport]
     p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
     return p
 
@@ -152,6 +170,23 @@ def test_bench_multi_gpu_leg_host_transport(cfg):
     assert ph["C_bytes"]["received"] == (S // 2 if cfg == "c3" else 0), ph
     if d["config"]["exchange"] != "pipe" and not d["config"]["exchange"].startswith("pipe"):
         assert set(ph["A_GBs_per_rank"]) == {"sent", "received", "per_link", "link_frac"}, ph
+
+
+@pytest.mark.parametrize("cfg", ["c3", "c4"])
+def test_bench_multi_gpu_leg_rccl_net(cfg):
+    """bench.py's N > 1 leg on RCCL communicators (2 ranks sharing the GPU,
+    RCCL's socket transport): every exchange variant -- COLL as
+    ncclAllToAll + ncclAllGather -- ran as itself with parity bit-exact."""
+    p = _bench_host(cfg, transport="rccl-net")
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = [x for x in p.stdout.splitlines() if x.startswith("{")]
+    assert len(line) == 1, p.stdout[-2000:]
+    d = json.loads(line[0])
+    assert d["parity"].startswith("bit-exact"), d
+    assert d["config"]["transport"] == "rccl-net"
+    tuning = d["config"]["exchange_tuning"]
+    assert all(v["parity"] for v in tuning.values()), tuning
+    assert tuning["coll"]["ran"] == "coll" and tuning["p2p"]["ran"] == "p2p", tuning
 
 
 @pytest.mark.parametrize("bad", ["coll@1", "p2p@0,pipe8@1"])
