@@ -447,6 +447,14 @@ def _fail_injected(name, rank):
     return any(x == "%s@%d" % (name, rank) for x in spec.split(",") if x)
 
 
+def _hang_injected(name, rank):
+    """MVX_BENCH_HANG=variant@rank: that rank never issues the checked step
+    of that exchange variant, so its peers' transfers wait forever (a test
+    of the hang path: variant timeout, communicator abort, a fresh one)"""
+    spec = os.environ.get("MVX_BENCH_HANG", "")
+    return any(x == "%s@%d" % (name, rank) for x in spec.split(",") if x)
+
+
 def _wait_stream(stream, seconds):
     """True once the stream drained, False after `seconds` (a hung transfer)"""
     t0 = time.perf_counter()
@@ -570,6 +578,8 @@ def run_multi(args, mvx, dev, world, rank, local):
         s = it[0] % sets
         it[0] += 1
         c = cur["comm"]
+        if it[0] == 1 and _hang_injected(cur["name"], rank):
+            return
         if coll == "allreduce":
             rc = c.allreduce_async(sendbuf[s], recvbuf[s], n, dtype, op, stream)
         else:

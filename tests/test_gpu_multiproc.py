@@ -9,6 +9,9 @@
 * RCCL over xGMI (mvx_comm_init): the same suite, plus the BASELINE
   multi-GPU shapes (C3, C4, C5) at full size, on p = 2, 4, 8 GPUs -- skipped
   where the box has fewer GPUs.
+* RCCL with ranks sharing the one GPU (rccl-net: each rank its own
+  NCCL_HOSTID, so RCCL's socket transport moves the bytes): the suites, the
+  bench leg, and the bench's hang path (ncclCommAbort, a fresh communicator).
 * bench.py under torchrun with the host transport: the multi-GPU leg
   (exchange tuning, parity against the CPU reference schedule, p-thread CPU
   baseline) end to end on one GPU.
@@ -123,13 +126,13 @@ def test_rccl_multirank_net_transport(world):
                 assert ran["pipe"].get("1", 0) > 0, ran
 
 
-def _bench_host(cfg, extra_env=None, world=2, transport="host"):
+def _bench_host(cfg, extra_env=None, world=2, transport="host", extra_args=()):
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
     env.update(extra_env or {})
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"),
            "--gpus", str(world), "--steps", "3", "--warmup", "1", "--tune-steps", "1", "--mib", "32",
-           "--config", cfg, "--transport", transport]
+           "--config", cfg, "--transport", transport] + list(extra_args)
     p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
     return p
 
@@ -187,6 +190,27 @@ def test_bench_multi_gpu_leg_rccl_net(cfg):
     tuning = d["config"]["exchange_tuning"]
     assert all(v["parity"] for v in tuning.values()), tuning
     assert tuning["coll"]["ran"] == "coll" and tuning["p2p"]["ran"] == "p2p", tuning
+
+
+def test_bench_survives_a_hung_variant_rccl_net():
+    """A variant whose checked step hangs (rank 1 never issues it: rank 0's
+    RCCL transfers wait for a peer that never comes, MVX_BENCH_HANG) is
+    detected by the variant timeout, every rank aborts its RCCL communicator
+    (ncclCommAbort) and builds a fresh one, and the later variants -- COLL
+    included -- still run on it with parity bit-exact."""
+    p = _bench_host("c3", {"MVX_BENCH_HANG": "pipe@1"}, transport="rccl-net",
+                    extra_args=["--variant-timeout", "15"])
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = [x for x in p.stdout.splitlines() if x.startswith("{")]
+    assert len(line) == 1, p.stdout[-2000:]
+    d = json.loads(line[0])
+    tuning = d["config"]["exchange_tuning"]
+    assert tuning["pipe"]["ms_per_step"] is None and "did not complete" in tuning["pipe"]["error"], tuning
+    assert "stayed blocked" not in tuning["pipe"]["error"], tuning
+    for v in ("p2p", "pipe2", "pipe8", "coll"):
+        assert tuning[v]["parity"] and tuning[v]["ms_per_step"], tuning
+    assert tuning["coll"]["ran"] == "coll", tuning
+    assert d["parity"].startswith("bit-exact"), d
 
 
 @pytest.mark.parametrize("bad", ["coll@1", "p2p@0,pipe8@1"])
