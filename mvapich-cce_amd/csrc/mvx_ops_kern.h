@@ -306,8 +306,16 @@ __device__ __forceinline__ u32x4 ld(const u32x4 *p)
 template <int NT>
 __device__ __forceinline__ void st(u32x4 *p, u32x4 v)
 {
-    if constexpr (NT) __builtin_nontemporal_store(v, p);
-    else *p = v;
+    if constexpr (NT) {
+        // the empty asm makes the stored dwordx4 opaque: where the value was
+        // assembled from narrower fields (MPI_LONG_DOUBLE_INT's 16-bit sign
+        // and exponent) the optimiser otherwise re-typed the store and
+        // dropped its non-temporal hint (the x87 trees stored cached)
+        __asm__("" : "+v"(v));
+        __builtin_nontemporal_store(v, p);
+    } else {
+        *p = v;
+    }
 }
 
 template <typename T, int NT>

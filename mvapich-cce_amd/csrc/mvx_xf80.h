@@ -266,28 +266,48 @@ XF_FN xf80 mul(xf80 a, xf80 b)
     return round_pack(a, s, e, P);
 }
 
-// x87 compare: -1, 0, 1, or 2 = unordered (NaN or invalid encoding).
-// Branch-free: unordered is every class from K_QNAN up (exponent 0x7fff
-// except an infinity, or an unnormal); magnitudes order by (exponent, with
-// denormals and pseudo-denormals at 1; significand), zero below all; one
-// sign flip.  The MPI_MAX / MIN / MAXLOC / MINLOC trees run one of these per
-// step, and the branchy form left more scalar exec-mask work than vector work
-// in their loop (tools: --save-temps of mvx_ops_loc.hip).
-XF_FN int cmp(const xf80 &a, const xf80 &b)
+// An ordered operand as an unsigned 81-bit key (hi: 17 bits, lo: 64) that
+// sorts as the x87 orders the values: the magnitude is (exponent, with
+// denormals and pseudo-denormals at 1 and zero at 0; significand); a
+// negative nonzero value takes the complement of its magnitude, every other
+// value has bit 16 of hi set -- so -0 and +0 share one key, and equal keys
+// are exactly the x87's equal values.  `u`: unordered (a NaN, or an invalid
+// encoding: exponent 0x7fff except an infinity, or an unnormal).
+struct xkey {
+    uint32_t hi;
+    uint64_t lo;
+    uint32_t u;
+};
+
+// Bitwise forms throughout (no && / || / ?: on the class tests): the
+// short-circuit forms became exec-mask branches around every step of the
+// MPI_MAX / MIN / MAXLOC / MINLOC trees (--save-temps of mvx_ops_loc.hip).
+XF_FN xkey key(const xf80 &a)
 {
-    const uint32_t ea = a.se & 0x7fff, eb = b.se & 0x7fff;
-    const bool ja = (a.m >> 63) != 0, jb = (b.m >> 63) != 0;
-    const bool ua = ea == 0x7fff ? !(ja && (a.m << 1) == 0) : (ea != 0 && !ja);
-    const bool ub = eb == 0x7fff ? !(jb && (b.m << 1) == 0) : (eb != 0 && !jb);
-    const bool za = ea == 0 && a.m == 0, zb = eb == 0 && b.m == 0;
-    const uint32_t xa = za ? 0u : (ea ? ea : 1u), xb = zb ? 0u : (eb ? eb : 1u);
-    const bool gt = xa > xb || (xa == xb && a.m > b.m);
-    const bool eq = xa == xb && a.m == b.m;
-    const uint32_t sa = a.se >> 15, sb = b.se >> 15;
-    const int c = eq ? 0 : (gt != (sa != 0) ? 1 : -1);      // magnitude order, sign applied
-    const int r = (za && zb) ? 0 : (sa != sb ? (sa ? -1 : 1) : c);
-    return (ua || ub) ? 2 : r;
+    const uint32_t e = a.se & 0x7fff;
+    const uint32_t j = (uint32_t)(a.m >> 63);
+    const uint32_t frac = (uint32_t)((a.m << 1) != 0);
+    const uint32_t x = e | (uint32_t)((e == 0) & (a.m != 0));          // 0 only for a zero
+    const uint32_t neg = (uint32_t)(a.se >> 15) & (uint32_t)(x != 0);
+    const uint64_t mask = 0ull - (uint64_t)neg;
+    xkey k;
+    k.hi = (x | 0x10000u) ^ ((uint32_t)mask & 0x1ffffu);
+    k.lo = a.m ^ mask;
+    k.u = ((j ^ 1u) & (uint32_t)(e != 0)) | ((uint32_t)(e == 0x7fff) & frac);
+    return k;
 }
+
+// x87 compare: -1, 0, 1, or 2 = unordered
+XF_FN int cmp_keys(const xkey &a, const xkey &b)
+{
+    const uint32_t hgt = a.hi > b.hi, heq = a.hi == b.hi;
+    const uint32_t gt = hgt | (heq & (uint32_t)(a.lo > b.lo));
+    const uint32_t eq = heq & (uint32_t)(a.lo == b.lo);
+    const int c = (int)gt - (int)((gt | eq) ^ 1u);
+    return (a.u | b.u) ? 2 : c;
+}
+
+XF_FN int cmp(const xf80 &a, const xf80 &b) { return cmp_keys(key(a), key(b)); }
 
 XF_FN bool truth(const xf80 &a)                       // `a != 0`, unordered is true
 {
