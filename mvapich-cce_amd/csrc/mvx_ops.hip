@@ -138,6 +138,20 @@ static unsigned g_last_blocks;
 static size_t g_last_lds;
 static const void *g_last_fn;
 
+// dynamic LDS per block that leaves room for `cap` blocks per CU and not one
+// more (the kernels do not touch it): the middle of the range,
+// 2 * LDS / (2 * cap + 1), clear of the allocator's rounding at the edges; at
+// most 64 KiB (no function attribute needed).  gfx950: 160 KiB of LDS per CU
+// (the runtime's per-multiprocessor attribute reports the 64 KiB per-block
+// limit instead)
+static size_t cap_lds(int cap)
+{
+    const size_t lds_per_cu = 160 * 1024;
+    if (cap < 2) return 0;
+    const size_t b = (lds_per_cu * 2 / (size_t)(2 * cap + 1)) & ~(size_t)1023;
+    return b > 64 * 1024 ? 64 * 1024 : b;
+}
+
 static void init_env()
 {
     static int done = 0;
@@ -154,18 +168,10 @@ static void init_env()
     e = getenv("MVX_NO_BODY");
     if (e && atoi(e) == 1) g_no_body = 1;
     const char *caps[FAM_N] = {"MVX_CAP_APPLY", "MVX_CAP_PROG", "MVX_CAP_TREE"};
-    // gfx950: 160 KiB of LDS per CU (the runtime's per-multiprocessor
-    // attribute reports the 64 KiB per-block limit instead)
-    const int lds_per_cu = 160 * 1024;
     for (int f = 0; f < FAM_N; ++f) {
         e = getenv(caps[f]);
         if (e) g_cap[f] = atoi(e);
-        // dynamic LDS per block that leaves room for g_cap blocks per CU and
-        // not one more (the kernels do not touch it): the middle of the
-        // range, 2 * LDS / (2 * cap + 1), clear of the allocator's rounding
-        // at the edges; at most 64 KiB (no function attribute needed)
-        g_cap_lds[f] = g_cap[f] >= 2 ? ((size_t)lds_per_cu * 2 / (size_t)(2 * g_cap[f] + 1)) & ~(size_t)1023 : 0;
-        if (g_cap_lds[f] > 64 * 1024) g_cap_lds[f] = 64 * 1024;
+        g_cap_lds[f] = cap_lds(g_cap[f]);
     }
 }
 
@@ -206,12 +212,13 @@ static int launch(const KSet *ks, const KFam &F, Params &P, hipStream_t stream)
         for (int q = 0; q < P.k; ++q) B.src[q] = reinterpret_cast<const u32x4 *>(P.src[q]);
         B.dst = reinterpret_cast<u32x4 *>(P.dst);
         B.nvec = P.nvec;
-        long work = (P.nvec + F.body_unroll * 256 - 1) / (F.body_unroll * 256);
+        long work = (P.nvec * F.body_units + F.body_unroll * 256 - 1) / (F.body_unroll * 256);
         const unsigned blocks = (unsigned)(work < g_block_cap ? work : g_block_cap);
         void *bargs[] = {&B};
-        hipError_t e = hipLaunchKernel(F.body, dim3(blocks), dim3(256), bargs, 0, stream);
+        const size_t blds = cap_lds(F.body_cap);
+        hipError_t e = hipLaunchKernel(F.body, dim3(blocks), dim3(256), bargs, blds, stream);
         g_last_blocks = blocks;
-        g_last_lds = 0;
+        g_last_lds = blds;
         g_last_fn = F.body;
         snprintf(g_last_buf, sizeof g_last_buf, "%s_k%d_nt", ks->name, P.k);
         g_last = g_last_buf;

@@ -71,11 +71,11 @@ static_assert(sizeof(xf80) == 16 && sizeof(pxi) == 32, "");
 template <typename B> struct pp;
 
 // the x87 types: every op is dozens of integer instructions, so their
-// combines are ALU-bound and keep full occupancy (no body kernels, no
+// combines are ALU-bound and keep full occupancy (no k_tree_body, no
 // residency cap: the 8-leaf x87 SUM tree ran 109.7 us at 2 blocks per CU
-// against 74.4 us uncapped, profiles/r02/bench_kernels_x87.jsonl; an
-// uncapped body kernel with the short argument block ran the MAXLOC tree at
-// 114 us against 108-112 us through k_combine, profiles/r03/bench_kernels_x87_ab.jsonl)
+// against 74.4 us uncapped, profiles/r02/bench_kernels_x87.jsonl).  The
+// MPI_LONG_DOUBLE_INT MAXLOC / MINLOC trees have their own body kernel,
+// k_pxi_loc_body (one element per lane pair).
 template <typename T> struct alu_heavy { static constexpr bool v = false; };
 template <> struct alu_heavy<xf80> { static constexpr bool v = true; };
 template <> struct alu_heavy<pxi> { static constexpr bool v = true; };
@@ -550,6 +550,72 @@ k_chain_body(const BodyParams P)
     }
 }
 
+// MPI_LONG_DOUBLE_INT MAXLOC / MINLOC (global_ops.c:1365-1378 / 1605-1618)
+// as lane PAIRS.  An element is 32 bytes: the x87 value in the first 16
+// (significand, sign / exponent, slot padding), the int loc and padding in
+// the second.  One element per lane made every load instruction touch 2 KiB
+// with half of each 128-byte line (the tree ran at 65 % of HBM peak whatever
+// its occupancy, profiles/r03/bench_kernels_x87_cap_sweep.jsonl); here lane
+// 2j holds the value half of element j and lane 2j+1 its loc half, so each
+// load and store is 1 KiB contiguous per wave.  The even lane compares, one
+// DPP quad permutation hands the result to its odd partner, and each lane
+// selects its own half: value and sign / exponent from the winner with a's
+// slot padding (even), loc as the reference sets it (odd).
+template <bool MIN>
+__device__ __forceinline__ u32x4 loc_half(u32x4 a, u32x4 b, bool odd)
+{
+    xf80 va, vb;
+    __builtin_memcpy(&va, &a, sizeof va);
+    __builtin_memcpy(&vb, &b, sizeof vb);
+    int c = xf::cmp(va, vb);                                  // meaningful in even lanes
+    c = __builtin_amdgcn_update_dpp(0, c, 0xA0, 0xF, 0xF, false);   // quad_perm [0, 0, 2, 2]
+    const bool take = c == (MIN ? 1 : -1);
+    const int32_t la = (int32_t)a.x, lb = (int32_t)b.x;
+    const uint32_t lsel = c == 0 ? (uint32_t)(la < lb ? la : lb) : (take ? b.x : a.x);
+    u32x4 r = a;
+    r.x = odd ? lsel : (take ? b.x : a.x);
+    r.y = odd ? a.y : (take ? b.y : a.y);
+    r.z = odd ? a.z : (take ? ((b.z & 0xffffu) | (a.z & 0xffff0000u)) : a.z);
+    return r;
+}
+
+// the full tree over KMAX leaves; BodyParams.nvec counts elements (32 B)
+template <int O, int KMAX, int U>
+__global__ void __launch_bounds__(256)
+k_pxi_loc_body(const BodyParams P)
+{
+    // the launch may reserve dynamic LDS to cap resident blocks per CU
+    extern __shared__ char lds_cap[];
+    if (P.nvec < 0) lds_cap[threadIdx.x] = 0;
+    constexpr bool MIN = O == OMINLOC;
+    const long n = 2 * P.nvec;                 // 16-byte halves; even, so pairs stay whole
+    const bool odd = threadIdx.x & 1;
+    const long nthr = (long)gridDim.x * 256;
+    for (long c0 = (long)blockIdx.x * (256 * U) + threadIdx.x; c0 < n; c0 += nthr * U) {
+        u32x4 x[U][KMAX];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const long c = c0 + (long)u * 256;
+            if (c < n)
+#pragma unroll
+                for (int q = 0; q < KMAX; ++q) x[u][q] = ld<1>(P.src[q] + c);
+        }
+        // every lane runs the tree (lanes past the end on unloaded
+        // registers, never stored), so the DPP partner is always active
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int h = 1; h < KMAX; h <<= 1)
+#pragma unroll
+                for (int q = 0; q + h < KMAX; q += 2 * h) x[u][q] = loc_half<MIN>(x[u][q], x[u][q + h], odd);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const long c = c0 + (long)u * 256;
+            if (c < n) st<BODY_ST_NT>(P.dst + c, x[u][0]);
+        }
+    }
+}
+
 }  // namespace mvx
 
 // ---------------------------------------------------------------------------
@@ -622,6 +688,8 @@ struct KFam {
     SymFn body_sym;
     int body_unroll;
     int body_k;            // the body kernel's leaf count (launches with other k never use it)
+    int body_units;        // 16-byte units one body thread moves per element (k_pxi_loc_body: 2)
+    int body_cap;          // resident blocks per CU by a dynamic LDS reservation (0: none)
 };
 
 struct KSet {
@@ -635,6 +703,20 @@ struct KSet {
     const char *name;
 };
 
+template <int O, int KMAX, int U>
+static const char *ksym_pxi_body()
+{
+    static char buf[96];
+    if (!buf[0]) snprintf(buf, sizeof buf, "k_pxi_loc_body<%d, %d, %d>", O, KMAX, U);
+    return buf;
+}
+
+static inline int env_int(const char *name, int dflt)
+{
+    const char *e = getenv(name);
+    return e ? atoi(e) : dflt;
+}
+
 template <int O, typename T, int KMAX, int U0, int U1, int PROG>
 static KFam kfam(int fam)
 {
@@ -646,11 +728,26 @@ static KFam kfam(int fam)
     f.unroll[0] = U0;
     f.unroll[1] = U1;
     f.fam = (fam == FAM_TREE && alu_heavy<T>::v) ? FAM_PROG : fam;
+    f.body_units = 1;
+    f.body_cap = 0;
     if constexpr (PROG == 1 && !alu_heavy<T>::v) {
         f.body = (const void *)&k_tree_body<O, T, KMAX, U1>;
         f.body_sym = &ksym_body<O, T, KMAX, U1>;
         f.body_unroll = U1;
         f.body_k = KMAX;
+    } else if constexpr (PROG == 1 && std::is_same<T, pxi>::value && (O == OMAXLOC || O == OMINLOC)) {
+        // one element per lane pair at 4 resident blocks per CU: 8 x 64 MiB
+        // MAXLOC tree 96.4 us (78 % of HBM peak) against 115-117 us one
+        // element per lane; U = 2 at 3 blocks 96.2-96.9, uncapped 99-101
+        // (profiles/r03/bench_kernels_x87_pair_sweep.jsonl); MVX_PXI_U /
+        // MVX_PXI_CAP for A/B runs
+        const int u = env_int("MVX_PXI_U", 1);
+        f.body = u == 2 ? (const void *)&k_pxi_loc_body<O, KMAX, 2> : (const void *)&k_pxi_loc_body<O, KMAX, 1>;
+        f.body_sym = u == 2 ? &ksym_pxi_body<O, KMAX, 2> : &ksym_pxi_body<O, KMAX, 1>;
+        f.body_unroll = u == 2 ? 2 : 1;
+        f.body_k = KMAX;
+        f.body_units = 2;
+        f.body_cap = env_int("MVX_PXI_CAP", 4);
     } else {
         f.body = nullptr;
         f.body_sym = nullptr;

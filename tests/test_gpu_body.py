@@ -76,3 +76,23 @@ def test_launch_residency_reported(mvx):
     _run(mvx, 102, 10, 2, SHAPE_TREE, NT_ELEMS * 8)
     blocks, lds, occ = mvx.last_launch()
     assert occ == 8 and lds == 0
+
+
+@pytest.mark.parametrize("k", [4, 8])
+@pytest.mark.parametrize("op", [110, 111])
+def test_long_double_int_loc_pair_body(mvx, op, k):
+    """MAXLOC / MINLOC trees on MPI_LONG_DOUBLE_INT (32-byte elements): large
+    aligned launches run the lane-pair body (k_pxi_loc_body: lane 2j the x87
+    value half, lane 2j+1 the loc half, the compare handed over by DPP) --
+    bit for bit against the oracle's x87, ties, NaNs, invalid encodings and
+    slot padding included; a start off the 16-byte grid runs k_combine."""
+    n = 1 << 19                          # 16 MiB per leaf: a non-temporal launch
+    for seed in (0, 1):
+        sym, got, ref = _run(mvx, op, 22, k, SHAPE_TREE, n + seed * 4096, seed=seed)
+        assert sym.startswith("k_pxi_loc_body<"), sym
+        assert np.array_equal(got, ref)
+        # 4 resident blocks per CU (the dynamic LDS reservation)
+        assert mvx.last_launch()[2] == 4
+    sym, got, ref = _run(mvx, op, 22, k, SHAPE_TREE, n, offset=8, seed=2)
+    assert sym.startswith("k_combine<"), sym
+    assert np.array_equal(got, ref)
