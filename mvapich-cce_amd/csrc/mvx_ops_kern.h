@@ -567,11 +567,14 @@ __device__ __forceinline__ u32x4 loc_half(u32x4 a, u32x4 b, bool odd)
     xf80 va, vb;
     __builtin_memcpy(&va, &a, sizeof va);
     __builtin_memcpy(&vb, &b, sizeof vb);
-    int c = xf::cmp(va, vb);                                  // meaningful in even lanes
-    c = __builtin_amdgcn_update_dpp(0, c, 0xA0, 0xF, 0xF, false);   // quad_perm [0, 0, 2, 2]
-    const bool take = c == (MIN ? 1 : -1);
+    // meaningful in even lanes: 1 = b wins, 2 = equal values, 0 = keep a
+    const xf::xord o = xf::order(va, vb);
+    const bool win = !o.un & (MIN ? o.gt : !(o.gt | o.eq));
+    int code = win ? 1 : ((!o.un & o.eq) ? 2 : 0);
+    code = __builtin_amdgcn_update_dpp(0, code, 0xA0, 0xF, 0xF, false);   // quad_perm [0, 0, 2, 2]
+    const bool take = code == 1;
     const int32_t la = (int32_t)a.x, lb = (int32_t)b.x;
-    const uint32_t lsel = c == 0 ? (uint32_t)(la < lb ? la : lb) : (take ? b.x : a.x);
+    const uint32_t lsel = code == 2 ? (uint32_t)(la < lb ? la : lb) : (take ? b.x : a.x);
     u32x4 r = a;
     r.x = odd ? lsel : (take ? b.x : a.x);
     r.y = odd ? a.y : (take ? b.y : a.y);

@@ -276,38 +276,69 @@ XF_FN xf80 mul(xf80 a, xf80 b)
 struct xkey {
     uint32_t hi;
     uint64_t lo;
-    uint32_t u;
+    bool u;
 };
 
-// Bitwise forms throughout (no && / || / ?: on the class tests): the
-// short-circuit forms became exec-mask branches around every step of the
-// MPI_MAX / MIN / MAXLOC / MINLOC trees (--save-temps of mvx_ops_loc.hip).
+// The class tests are bools combined with & and | (never && / || / ?: on
+// them): on the device each stays a lane mask and combines in scalar
+// mask instructions, with no branch -- the short-circuit forms became
+// exec-mask branches around every step of the MPI_MAX / MIN / MAXLOC /
+// MINLOC trees, and integer 0 / 1 forms cost vector instructions
+// (--save-temps of mvx_ops_{cmp,loc}.hip).
 XF_FN xkey key(const xf80 &a)
 {
     const uint32_t e = a.se & 0x7fff;
-    const uint32_t j = (uint32_t)(a.m >> 63);
-    const uint32_t frac = (uint32_t)((a.m << 1) != 0);
-    const uint32_t x = e | (uint32_t)((e == 0) & (a.m != 0));          // 0 only for a zero
-    const uint32_t neg = (uint32_t)(a.se >> 15) & (uint32_t)(x != 0);
-    const uint64_t mask = 0ull - (uint64_t)neg;
+    const bool j = (a.m >> 63) != 0;
+    const bool ez = e == 0, mz = a.m == 0;
+    const uint32_t x = (ez & !mz) ? 1u : e;                     // 0 only for a zero
+    const bool neg = ((a.se & 0x8000) != 0) & !(ez & mz);
     xkey k;
-    k.hi = (x | 0x10000u) ^ ((uint32_t)mask & 0x1ffffu);
-    k.lo = a.m ^ mask;
-    k.u = ((j ^ 1u) & (uint32_t)(e != 0)) | ((uint32_t)(e == 0x7fff) & frac);
+    k.hi = neg ? (~x & 0xffffu) : (x | 0x10000u);
+    k.lo = neg ? ~a.m : a.m;
+    k.u = (!j & !ez) | ((e == 0x7fff) & ((a.m << 1) != 0));
     return k;
 }
 
-// x87 compare: -1, 0, 1, or 2 = unordered
-XF_FN int cmp_keys(const xkey &a, const xkey &b)
+// a against b: greater, equal, unordered (gt / eq meaningless when un)
+struct xord {
+    bool gt, eq, un;
+};
+
+XF_FN xord order(const xf80 &a, const xf80 &b)
 {
-    const uint32_t hgt = a.hi > b.hi, heq = a.hi == b.hi;
-    const uint32_t gt = hgt | (heq & (uint32_t)(a.lo > b.lo));
-    const uint32_t eq = heq & (uint32_t)(a.lo == b.lo);
-    const int c = (int)gt - (int)((gt | eq) ^ 1u);
-    return (a.u | b.u) ? 2 : c;
+    const xkey ka = key(a), kb = key(b);
+    const bool heq = ka.hi == kb.hi;
+    xord o;
+    o.gt = (ka.hi > kb.hi) | (heq & (ka.lo > kb.lo));
+    o.eq = heq & (ka.lo == kb.lo);
+    o.un = ka.u | kb.u;
+    return o;
 }
 
-XF_FN int cmp(const xf80 &a, const xf80 &b) { return cmp_keys(key(a), key(b)); }
+// x87 compare: -1, 0, 1, or 2 = unordered (NaN or invalid encoding), as
+// selects on the classes: unordered is every class from K_QNAN up (exponent
+// 0x7fff except an infinity, or an unnormal); magnitudes order by (exponent,
+// with denormals and pseudo-denormals at 1; significand), zero below all;
+// one sign flip.  MPI_MAX / MIN use this form: its class tests run largely
+// as scalar mask instructions, and the 8-leaf MAX tree measured 49.6-50.1 us
+// with it against 51.5-51.7 us through order() (profiles/r03/
+// bench_kernels_x87_ab.jsonl, bench_kernels_x87_pair_*.jsonl); the loc ops
+// use order(), whose compare result the lane-pair kernel hands across lanes.
+XF_FN int cmp(const xf80 &a, const xf80 &b)
+{
+    const uint32_t ea = a.se & 0x7fff, eb = b.se & 0x7fff;
+    const bool ja = (a.m >> 63) != 0, jb = (b.m >> 63) != 0;
+    const bool ua = ea == 0x7fff ? !(ja && (a.m << 1) == 0) : (ea != 0 && !ja);
+    const bool ub = eb == 0x7fff ? !(jb && (b.m << 1) == 0) : (eb != 0 && !jb);
+    const bool za = ea == 0 && a.m == 0, zb = eb == 0 && b.m == 0;
+    const uint32_t xa = za ? 0u : (ea ? ea : 1u), xb = zb ? 0u : (eb ? eb : 1u);
+    const bool gt = xa > xb || (xa == xb && a.m > b.m);
+    const bool eq = xa == xb && a.m == b.m;
+    const uint32_t sa = a.se >> 15, sb = b.se >> 15;
+    const int c = eq ? 0 : (gt != (sa != 0) ? 1 : -1);      // magnitude order, sign applied
+    const int r = (za && zb) ? 0 : (sa != sb ? (sa ? -1 : 1) : c);
+    return (ua || ub) ? 2 : r;
+}
 
 XF_FN bool truth(const xf80 &a)                       // `a != 0`, unordered is true
 {
@@ -343,13 +374,14 @@ struct pxi {
 template <bool MIN>
 XF_FN pxi loc(pxi a, pxi b)
 {
-    const int c = cmp(a.v, b.v);
-    const bool take = c == (MIN ? 1 : -1);
+    const xord o = order(a.v, b.v);
+    const bool take = !o.un & (MIN ? o.gt : !(o.gt | o.eq));
+    const bool same = !o.un & o.eq;
     const int32_t lmin = a.l < b.l ? a.l : b.l;
     pxi r = a;
     r.v.m = take ? b.v.m : a.v.m;
     r.v.se = take ? b.v.se : a.v.se;
-    r.l = c == 0 ? lmin : (take ? b.l : a.l);
+    r.l = same ? lmin : (take ? b.l : a.l);
     return r;
 }
 
