@@ -720,18 +720,27 @@ def run_multi(args, mvx, dev, world, rank, local):
         dist.barrier()
         t0 = time.perf_counter()
         terr = 0
+        issue = []
         for _ in range(args.tune_steps):      # every rank issues every step
+            t1 = time.perf_counter()
             try:
                 step()
             except RuntimeError:
                 terr = 1
+            issue.append(time.perf_counter() - t1)
         torch.cuda.synchronize()
         t[0] = time.perf_counter() - t0
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        # host time inside one collective call (plan, staging, RCCL enqueue
+        # and kernel launches; RCCL returns before the transfers end), the
+        # median over the tuning steps, MAX over ranks
+        hi = torch.tensor([statistics.median(issue)], dtype=torch.float64)
+        dist.all_reduce(hi, op=dist.ReduceOp.MAX)
         if agree(terr):
             entry.update(ms_per_step=None, parity=ok, error="an error return on some rank while tuning")
         else:
-            entry.update(ms_per_step=round(float(t.item()) * 1e3 / args.tune_steps, 4), parity=ok)
+            entry.update(ms_per_step=round(float(t.item()) * 1e3 / args.tune_steps, 4), parity=ok,
+                         host_issue_us=round(float(hi.item()) * 1e6, 1))
         tried[name] = entry
         # measure for the line: the first clean variant, then any that tuned
         # faster than the one measured (every rank decides alike: the tuning

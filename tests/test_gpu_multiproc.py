@@ -190,6 +190,7 @@ def test_bench_multi_gpu_leg_rccl_net(cfg):
     tuning = d["config"]["exchange_tuning"]
     assert all(v["parity"] for v in tuning.values()), tuning
     assert tuning["coll"]["ran"] == "coll" and tuning["p2p"]["ran"] == "p2p", tuning
+    assert all(v["host_issue_us"] > 0 for v in tuning.values()), tuning
 
 
 def test_bench_survives_a_hung_variant_rccl_net():
