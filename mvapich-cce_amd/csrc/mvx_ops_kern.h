@@ -303,15 +303,16 @@ __device__ __forceinline__ u32x4 ld(const u32x4 *p)
     else return *p;
 }
 
-template <int NT>
+// OPAQUE: an empty asm makes the stored dwordx4 opaque first.  Where the
+// value was assembled from narrower fields (the x87 types' 16-bit sign and
+// exponent) the optimiser otherwise re-typed the store and dropped its
+// non-temporal hint (the x87 MAXLOC / MINLOC trees stored cached); for the
+// other types the store already keeps it and their code stays as measured.
+template <int NT, bool OPAQUE = false>
 __device__ __forceinline__ void st(u32x4 *p, u32x4 v)
 {
     if constexpr (NT) {
-        // the empty asm makes the stored dwordx4 opaque: where the value was
-        // assembled from narrower fields (MPI_LONG_DOUBLE_INT's 16-bit sign
-        // and exponent) the optimiser otherwise re-typed the store and
-        // dropped its non-temporal hint (the x87 trees stored cached)
-        __asm__("" : "+v"(v));
+        if constexpr (OPAQUE) __asm__("" : "+v"(v));
         __builtin_nontemporal_store(v, p);
     } else {
         *p = v;
@@ -335,7 +336,7 @@ __device__ __forceinline__ void st_chunk(u32x4 *base, long c, const Chunk<T> &x)
     u32x4 r[CG<T>::w];
     __builtin_memcpy(r, &x, sizeof x);
 #pragma unroll
-    for (int w = 0; w < CG<T>::w; ++w) st<NT>(base + c * CG<T>::w + w, r[w]);
+    for (int w = 0; w < CG<T>::w; ++w) st<NT, alu_heavy<T>::v>(base + c * CG<T>::w + w, r[w]);
 }
 
 // PROG = 0: the program comes from the masks (any chain of trees over
@@ -614,7 +615,7 @@ k_pxi_loc_body(const BodyParams P)
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const long c = c0 + (long)u * 256;
-            if (c < n) st<BODY_ST_NT>(P.dst + c, x[u][0]);
+            if (c < n) st<BODY_ST_NT, true>(P.dst + c, x[u][0]);
         }
     }
 }
