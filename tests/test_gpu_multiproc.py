@@ -193,6 +193,32 @@ def test_bench_multi_gpu_leg_rccl_net(cfg):
     assert all(v["host_issue_us"] > 0 for v in tuning.values()), tuning
 
 
+def test_bench_full_size_eight_ranks_rccl_net():
+    """The driver's 8-GPU bench leg at the BASELINE sizes, with RCCL itself
+    carrying the bytes between 8 ranks that share the GPU (rccl-net): C3
+    (Allreduce SUM f32, 256 MiB per rank) with C5 (Allreduce MAXLOC
+    FLOAT_INT, 512 MiB per rank) in other_configs, every exchange variant
+    run as itself -- COLL as ncclAllToAll + in-place ncclAllGather at p = 8
+    -- and every rank's result bit-exact against the reference schedule."""
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", "8", "--steps", "2", "--warmup", "1", "--tune-steps", "1", "--transport", "rccl-net"]
+    p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=420)
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = [x for x in p.stdout.splitlines() if x.startswith("{")]
+    assert len(line) == 1, p.stdout[-2000:]
+    d = json.loads(line[0])
+    assert d["n_gpus"] == 8 and d["config"]["vector_bytes_per_rank"] == 256 << 20
+    assert d["parity"] == "bit-exact vs the reference schedule, all 8 ranks", d["parity"]
+    tuning = d["config"]["exchange_tuning"]
+    for name, v in tuning.items():
+        assert v["parity"] and v["ran"] == ("coll" if name == "coll" else name[:4]), (name, v)
+    (o,) = d["other_configs"]
+    assert o["config"] == "c5" and o["vector_bytes_per_rank"] == 512 << 20
+    assert o["parity"] == "bit-exact vs the reference schedule, all 8 ranks", o
+
+
 def test_bench_survives_a_hung_variant_rccl_net():
     """A variant whose checked step hangs (rank 1 never issues it: rank 0's
     RCCL transfers wait for a peer that never comes, MVX_BENCH_HANG) is
