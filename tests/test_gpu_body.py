@@ -15,10 +15,18 @@ pytestmark = pytest.mark.gpu
 NT_ELEMS = 4 << 20          # 16 MiB of f32 per leaf: a non-temporal launch at k >= 4
 
 
-def _run(mvx, op, dtype, k, shape, n, offset=0, folded=False, seed=0):
+def _run(mvx, op, dtype, k, shape, n, offset=0, folded=False, seed=0, ties=0.0):
     import torch
     E = mvx.dtype_info(dtype)[0]
     S = [T.rand_vec(dtype, n, 100 * seed + q) for q in range(k)]
+    if ties:
+        # equal values across leaves (x87 fields: the loc = min rule), a
+        # fraction `ties` of the elements of each leaf copied from the last
+        rng = np.random.default_rng(seed + 77)
+        for q in range(1, k):
+            sel = rng.random(n) < ties
+            cur, prev = S[q].view(np.uint8).reshape(n, -1), S[q - 1].view(np.uint8).reshape(n, -1)
+            cur[sel, :10] = prev[sel, :10]          # significand + sign / exponent
     F = [T.rand_vec(dtype, n, 100 * seed + 50 + q) if folded and q % 2 else None for q in range(k)]
     # device leaves at byte `offset` into their allocation (offset 4 breaks the
     # 16-byte body for 4-byte types: head elements, k_combine)
@@ -88,7 +96,7 @@ def test_long_double_int_loc_pair_body(mvx, op, k):
     slot padding included; a start off the 16-byte grid runs k_combine."""
     n = 1 << 19                          # 16 MiB per leaf: a non-temporal launch
     for seed in (0, 1):
-        sym, got, ref = _run(mvx, op, 22, k, SHAPE_TREE, n + seed * 4096, seed=seed)
+        sym, got, ref = _run(mvx, op, 22, k, SHAPE_TREE, n + seed * 4096, seed=seed, ties=0.3)
         assert sym.startswith("k_pxi_loc_body<"), sym
         assert np.array_equal(got, ref)
         # 4 resident blocks per CU (the dynamic LDS reservation)
