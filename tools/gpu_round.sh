@@ -2,7 +2,8 @@
 # One GPU-box session, by stage: smoke, tests, bench, PMC passes, kernel
 # trace, kernel micro-benches, host-buffer rates.  Every GPU step has its own
 # time limit; the chain stops at the first failure (no retries).
-#   tools/gpu_round.sh STAGE [pytest args]
+#   tools/gpu_round.sh STAGE [pytest args]   (STAGE: all smoke test bench pmc prof kernels host
+#   bench_ab kernels_ab pmc_kernels rccl_net)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
@@ -73,4 +74,11 @@ if [[ $STAGE == pmc_kernels ]]; then
   python3 tools/pmc_summary.py gpurun_out/pmck_f gpurun_out/pmck_w "k_tree_body<2, float, 8, 2>" sum_f32_k8_nt 33554432 301989888 gpurun_out/pmc_c3.json && \
   python3 tools/pmc_summary.py gpurun_out/pmck_f gpurun_out/pmck_w "k_chain_body<5, unsigned long, 4, 2>" band_u64_k4_nt 268435456 1342177280 gpurun_out/pmc_c4.json && \
   python3 tools/pmc_summary.py gpurun_out/pmck_f gpurun_out/pmck_w "k_tree_body<11, mvx::pfi, 8, 2>" maxloc_float_int_k8_nt 67108864 603979776 gpurun_out/pmc_c5.json || exit 1
+fi
+if [[ $STAGE == rccl_net ]]; then
+  # RCCL communicators whose ranks share the one GPU (NCCL_HOSTID per rank,
+  # RCCL's socket transport): the full-size bench legs and random sweeps
+  TRANSPORT=rccl-net tools/rehearse_full.sh c3 c4 || exit 1
+  MVX_MP_CASES=${MVX_MP_CASES:-300} tools/rccl_net_sweep.sh > gpurun_out/rccl_net_sweep.jsonl || { cat gpurun_out/rccl_net_sweep.jsonl; exit 1; }
+  cat gpurun_out/rccl_net_sweep.jsonl
 fi
