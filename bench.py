@@ -77,6 +77,8 @@ def parse():
     ap.add_argument("--variant-timeout", type=float, default=60.0,
                     help="N > 1: seconds one checked step of an exchange variant may take before the "
                          "variant counts as hung (its communicator is aborted and rebuilt)")
+    ap.add_argument("--no-native", action="store_true",
+                    help="N > 1: skip the RCCL-native reduction timed after the line (SURVEY.md 8(e) ablation)")
     ap.add_argument("--no-kernels", action="store_true",
                     help="N = 1: skip the C3 / C4 / C5 combine-kernel rates after the timed region")
     ap.add_argument("--transport", default="rccl", choices=["rccl", "host", "rccl-net"],
@@ -547,6 +549,51 @@ def run_extra(args, mvx, dev, world, rank, comm, exch_name, cfg, agree, stream):
     return out, 0
 
 
+def rccl_native(args, mvx, comm, cfg, n, sendbuf, world, dev, stream, agree, line_ms):
+    """After the line: RCCL's own reduction on the same communicator and the
+    same vectors -- ncclAllReduce (C3) or ncclReduceScatter (C4: over the
+    same int64 bytes as a SUM, RCCL has no BAND) -- the ablation SURVEY.md
+    8(e) keeps beside the path: RCCL's ring / tree order, not the
+    reference's, so it is a speed reference, never the line.  C5's pairs
+    have no RCCL reduction: None.  Returns (summary, worst status)."""
+    import torch
+    coll, dtype, _, E, _, _ = CONFIGS[cfg]
+    if dtype not in (MPI_FLOAT, MPI_LONG):
+        return None, 0
+    kind = mvx.COLL_ALLREDUCE if coll == "allreduce" else mvx.COLL_REDUCE_SCATTER
+    cnt = n if coll == "allreduce" else n // world
+    out = torch.empty(cnt * E, dtype=torch.uint8, device=dev)
+
+    def step():
+        rc = comm.rccl_native(kind, sendbuf, out, cnt, dtype, stream)
+        if rc:
+            raise RuntimeError("mvx_comm_rccl_native rc=%d" % rc)
+
+    try:
+        step()
+        status = 0 if _wait_stream(stream, args.variant_timeout) else 2
+    except RuntimeError:
+        status = 1
+    worst = agree(status)
+    res = {"op": "ncclAllReduce(ncclSum)" if coll == "allreduce" else "ncclReduceScatter(ncclSum)",
+           "note": "RCCL's own reduction on the same communicator and vectors (SURVEY.md 8(e) ablation): "
+                   "its ring / tree order is not the reference's and it has no BAND, so this is a speed "
+                   "reference for the exchange, never the line"}
+    if worst:
+        res["error"] = "an error return on some rank" if worst == 1 else "the checked step did not complete"
+        return res, worst
+    times = timed(args, step, stream, world)
+    sec = times["t_job"] / args.steps
+    p = world
+    nbytes = n * E
+    busbw = (2 if coll == "allreduce" else 1) * (p - 1) / p * nbytes / sec / 1e9
+    peak = min(p - 1, 7) * XGMI_LINK_GBS
+    res.update(ms_per_step=round(sec * 1e3, 5), busbw_GBs=round(busbw, 1), frac=round(busbw / peak, 4),
+               line_over_native=round(line_ms / (sec * 1e3), 3))
+    del out
+    return res, 0
+
+
 def run_multi(args, mvx, dev, world, rank, local):
     import torch
     import torch.distributed as dist
@@ -774,6 +821,14 @@ def run_multi(args, mvx, dev, world, rank, local):
             break
     if others:
         out["other_configs"] = others
+    if not aborted and not args.no_native and args.transport != "host":
+        nat, worst = rccl_native(args, mvx, cur["comm"], cfg, n, sendbuf[0], world, dev, stream, agree,
+                                 out["ms_per_step"])
+        if nat is not None:
+            out["rccl_native"] = nat
+        if worst == 2:
+            cur["comm"].abort()
+            aborted = True
     if not aborted:
         cur["comm"].free()
     return out

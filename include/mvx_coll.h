@@ -102,6 +102,16 @@ int mvx_comm_last_exchange(MPI_Comm comm, int *mode);
  * handle is freed as by mvx_comm_free; the staging memory is not (work
  * queued behind the aborted transfers may still read it). */
 int mvx_comm_abort(MPI_Comm *comm);
+/* Ablation only: RCCL's own ncclAllReduce (coll =
+ * MVX_COLL_ALLREDUCE, count elements) or ncclReduceScatter (coll =
+ * MVX_COLL_REDUCE_SCATTER, count elements per rank) with ncclSum on the
+ * communicator's RCCL handle, stream-ordered.  RCCL's combine order is not
+ * the reference's (floats differ in the last bits) and it has no BAND /
+ * MAXLOC: never a substitute for MPI_Allreduce / MPI_Reduce_scatter.
+ * MPI_FLOAT, MPI_DOUBLE, MPI_INT, MPI_LONG, MPI_LONG_LONG_INT; MPI_ERR_COMM
+ * on a communicator without RCCL (virtual, caller transport). */
+int mvx_comm_rccl_native(MPI_Comm comm, int coll, const void *sendbuf, void *recvbuf, size_t count,
+                         MPI_Datatype dt, void *stream);
 /* Per-phase timing (diagnostics): with timing on, each device-buffer call
  * records HIP events on its stream around phase A (exchange), B (combine)
  * and C (distribution).  mvx_comm_phase_times waits for the last timed call

@@ -166,6 +166,13 @@ class Comm:
     def set_stream(self, stream=None):
         return coll().mvx_comm_set_stream(self.handle, stream_handle(stream))
 
+    def rccl_native(self, coll_kind, sendbuf, recvbuf, count, dtype, stream=None):
+        """Ablation only: RCCL's own ncclAllReduce / ncclReduceScatter
+        (ncclSum) on this communicator (mvx_comm_rccl_native) -- not the
+        reference's combine order; never a substitute for the MPI calls."""
+        return coll().mvx_comm_rccl_native(self.handle, coll_kind, addr(sendbuf), addr(recvbuf), count, dtype,
+                                           stream_handle(stream))
+
     def reserve(self, nbytes):
         return coll().mvx_comm_reserve(self.handle, nbytes)
 

@@ -386,6 +386,31 @@ int mvx_comm_last_exchange(MPI_Comm comm, int *mode)
     return MPI_SUCCESS;
 }
 
+/* RCCL's own reduction on this communicator's RCCL handle, for the
+ * ablation SURVEY.md 8(e) keeps beside the path: ncclAllReduce /
+ * ncclReduceScatter with ncclSum, RCCL's ring / tree order -- not the
+ * reference's, so not bit-exact for floats, and no BAND / MAXLOC.  The MPI
+ * entry points never call it; bench.py times it after its line. */
+int mvx_comm_rccl_native(MPI_Comm comm, int coll, const void *sendbuf, void *recvbuf, size_t count,
+                         MPI_Datatype dt, void *stream)
+{
+    hipStream_t st = (hipStream_t)stream;
+    mvx_comm_t *c = get_comm(comm);
+    ncclDataType_t t;
+    ncclResult_t r;
+    if (!c) return ERR_COMM_NULL_CODE;
+    if (c->local || c->has_ops || !c->nccl) return MPI_ERR_COMM;
+    if (dt == MPI_FLOAT) t = ncclFloat32;
+    else if (dt == MPI_DOUBLE) t = ncclFloat64;
+    else if (dt == MPI_INT) t = ncclInt32;
+    else if (dt == MPI_LONG || dt == MPI_LONG_LONG_INT) t = ncclInt64;
+    else return MPI_ERR_TYPE;
+    if (coll == MVX_COLL_ALLREDUCE) r = ncclAllReduce(sendbuf, recvbuf, count, t, ncclSum, c->nccl, st);
+    else if (coll == MVX_COLL_REDUCE_SCATTER) r = ncclReduceScatter(sendbuf, recvbuf, count, t, ncclSum, c->nccl, st);
+    else return MPI_ERR_ARG;
+    return r == ncclSuccess ? MPI_SUCCESS : MPI_ERR_OTHER;
+}
+
 /* ---- per-phase timing of device calls -----------------------------------
  * With timing on, every device-buffer call records four events on its
  * stream: before phase A, after A, after B, after C (the pipelined variant,

@@ -162,6 +162,7 @@ def test_bench_multi_gpu_leg_host_transport(cfg):
     assert d["config"]["exchange_ran"] == tuning[d["config"]["exchange"]]["ran"]
     assert d["cpu_baseline"]["cores"] == 2
     assert d["config"]["transport"] == "host"
+    assert "rccl_native" not in d           # no RCCL handle under the host transport
     ph = d["roofline"]["phases"]
     assert ph["total_ms"] > 0, ph
     S = d["config"]["vector_bytes_per_rank"]
@@ -191,6 +192,10 @@ def test_bench_multi_gpu_leg_rccl_net(cfg):
     assert all(v["parity"] for v in tuning.values()), tuning
     assert tuning["coll"]["ran"] == "coll" and tuning["p2p"]["ran"] == "p2p", tuning
     assert all(v["host_issue_us"] > 0 for v in tuning.values()), tuning
+    # RCCL's own reduction on the same communicator, timed after the line
+    nat = d["rccl_native"]
+    assert nat["op"] == ("ncclAllReduce(ncclSum)" if cfg == "c3" else "ncclReduceScatter(ncclSum)"), nat
+    assert nat["ms_per_step"] > 0 and nat["line_over_native"] > 0, nat
 
 
 def test_bench_full_size_eight_ranks_rccl_net():
