@@ -46,9 +46,14 @@ CONFIGS = {
 EXCH = {"p2p": (0, 0), "pipe": (1, 4), "pipe2": (1, 2), "pipe8": (1, 8), "coll": (2, 0)}
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU).  Under torchrun it must equal WORLD_SIZE; without a launcher "
+                         "(no WORLD_SIZE) N > 1 starts N worker processes itself (launch())")
+    ap.add_argument("--launch-grace", type=float, default=30.0,
+                    help="self-launched N > 1: seconds the other workers get after one fails before they "
+                         "are killed")
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default=None, choices=["c2", "c3", "c4", "c5"],
@@ -86,7 +91,160 @@ def parse():
                          "share a GPU, bytes move through RCCL's own socket transport (each rank "
                          "names itself a separate host).  Both test the multi-GPU leg on a 1-GPU "
                          "box; neither is a performance configuration")
-    return ap.parse_args()
+    return ap.parse_args(argv)
+
+
+# ------------------------------------------------------------ wall clock --
+
+class Stages:
+    """Wall seconds per stage of this process, contiguous from the process's
+    creation (psutil): the stages partition the wall clock up to the last
+    mark, interpreter start-up and imports included, so a run that outlasts
+    a timeout says where the time went.  Rank 0 also prints each mark to
+    stderr (a long multi-GPU run keeps saying it is alive)."""
+
+    def __init__(self, verbose=False):
+        try:
+            import psutil
+            self.t0 = psutil.Process().create_time()
+        except Exception:            # no psutil: from here on
+            self.t0 = time.time()
+        self.last = self.t0
+        self.s = {}
+        self.verbose = verbose
+
+    def mark(self, name):
+        now = time.time()
+        self.s[name] = round(self.s.get(name, 0.0) + now - self.last, 3)
+        self.last = now
+        if self.verbose:
+            sys.stderr.write("bench: %-28s %8.2f s (wall %.1f s)\n" % (name, self.s[name], now - self.t0))
+            sys.stderr.flush()
+
+    def report(self):
+        now = time.time()
+        return {"stage_s": dict(self.s), "wall_s": round(now - self.t0, 3),
+                "unaccounted_s": round(now - self.last, 3)}
+
+
+ENV_PREFIXES = ("NCCL_", "RCCL_", "MVX_", "HSA_", "HIP_VISIBLE", "ROCR_VISIBLE", "CUDA_VISIBLE",
+                "GPU_MAX_HW_QUEUES", "TORCH_NCCL")
+
+
+def env_echo(env=None):
+    """The RCCL / HIP / MVX knobs this run saw (DESIGN.md section 6 names
+    the ones a node run needs: none beyond the image's)."""
+    env = os.environ if env is None else env
+    return {k: env[k] for k in sorted(env) if k.startswith(ENV_PREFIXES)}
+
+
+# --------------------------------------------------------------- launcher --
+
+def decide_launch(gpus, env):
+    """What main() does with --gpus under this environment:
+    ("single", 1) -- N = 1 in this process; ("self", N) -- no launcher set
+    WORLD_SIZE and N > 1: start N workers (launch()); ("worker", W) -- a
+    launcher (torchrun, or launch() itself) set WORLD_SIZE = W and --gpus is
+    absent or equal; ("mismatch", msg) -- --gpus names another world size."""
+    ws = env.get("WORLD_SIZE")
+    if ws is None:
+        n = 1 if gpus is None else gpus
+        if n < 1:
+            return "mismatch", "--gpus %d: need at least 1" % n
+        return ("self", n) if n > 1 else ("single", 1)
+    w = int(ws)
+    if gpus is not None and gpus != w:
+        return "mismatch", "--gpus %d but the launcher started WORLD_SIZE=%d ranks" % (gpus, w)
+    return ("worker", w) if w > 1 else ("single", 1)
+
+
+def worker_env(base, rank, n, port):
+    """The environment of self-launched worker `rank` of n (torchrun's names)."""
+    env = dict(base)
+    env.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+               GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), MVX_BENCH_LAUNCHER="self")
+    return env
+
+
+def _rc_of(rc):
+    return 128 - rc if rc < 0 else rc      # a signal -> 128 + signo, as a shell reports it
+
+
+def launch(args, n, argv):
+    """--gpus N > 1 with no WORLD_SIZE: one worker process per GPU, started
+    before this process touches the GPU (it never does), never by exec.
+    Rank 0's stdout is read here; its JSON line gets a "launch" entry (this
+    process's wall clock around the whole job, the workers' exit codes) and
+    is printed.  If a worker fails the others get --launch-grace seconds,
+    then are killed.  Exit code: the workers' worst."""
+    import signal
+    import socket
+    import subprocess
+    import threading
+    if args.transport == "rccl":
+        import torch          # counting devices does not initialise the GPU
+        have = torch.cuda.device_count()
+        if have < n:
+            sys.stderr.write("bench: --gpus %d over RCCL needs %d GPUs, this box has %d (RCCL refuses two "
+                             "ranks on one GPU; --transport rccl-net or host shares one)\n" % (n, n, have))
+            return 2
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    t0 = time.time()
+    cmd = [sys.executable, os.path.abspath(__file__)] + list(argv)
+
+    def die_with_parent():
+        try:
+            import ctypes
+            ctypes.CDLL("libc.so.6").prctl(1, signal.SIGKILL)   # PR_SET_PDEATHSIG
+        except Exception:
+            pass
+
+    procs = [subprocess.Popen(cmd, env=worker_env(os.environ, r, n, port),
+                              stdout=subprocess.PIPE if r == 0 else None, preexec_fn=die_with_parent)
+             for r in range(n)]
+    out0 = []
+    reader = threading.Thread(target=lambda: out0.extend(procs[0].stdout.read().decode().splitlines()),
+                              daemon=True)
+    reader.start()
+
+    def stop(signum, frame):
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+        sys.exit(128 + signum)
+
+    old = {s: signal.signal(s, stop) for s in (signal.SIGTERM, signal.SIGINT)}
+    failed_at = None
+    try:
+        while any(p.poll() is None for p in procs):
+            if failed_at is None and any(p.poll() not in (None, 0) for p in procs):
+                failed_at = time.time()
+            if failed_at is not None and time.time() - failed_at > args.launch_grace:
+                for p in procs:
+                    if p.poll() is None:
+                        p.kill()
+            time.sleep(0.1)
+    finally:
+        for s, h in old.items():
+            signal.signal(s, h)
+    reader.join(timeout=10)
+    rcs = [p.returncode for p in procs]
+    wall = time.time() - t0
+    for line in out0:
+        if line.startswith("{"):
+            try:
+                d = json.loads(line)
+            except ValueError:
+                print(line, flush=True)
+                continue
+            d["launch"] = {"mode": "self (bench.py --gpus %d without a launcher: %d worker processes)" % (n, n),
+                           "workers": n, "wall_s": round(wall, 3), "worker_rcs": rcs}
+            print(json.dumps(d), flush=True)
+        else:
+            print(line, flush=True)
+    return max(_rc_of(rc) for rc in rcs)
 
 
 def _cpu_model():
@@ -220,7 +378,7 @@ def prewarm(args, step):
             "note": "untimed steps before the W warmup steps (clock ramp-up); not in value"}
 
 
-def run_single(args, mvx, dev):
+def run_single(args, mvx, dev, clock):
     import torch
     nbytes = (args.mib or 256) * MIB
     n = nbytes // 4
@@ -240,8 +398,11 @@ def run_single(args, mvx, dev):
 
     # from input synthesis to the last timed step the GPU never idles: the
     # host-side parity check and the CPU leg run after the timed region
+    torch.cuda.synchronize()
+    clock.mark("inputs")
     warm = prewarm(args, step)
     times = timed(args, step, stream, 1)
+    clock.mark("timed steps")
     # cpu_baseline leg, part 1: the reference op on the same inputs (checker)
     parity = None
     if keep is not None:
@@ -271,6 +432,9 @@ def run_single(args, mvx, dev):
         out["cpu_baseline"] = cpu_baseline_op(nbytes, args.cpu_seconds)
     if not args.no_kernels:
         out["combine_kernels"] = combine_kernels(mvx)
+    clock.mark("parity, cpu baseline, combine kernels")
+    out["env"] = env_echo()
+    out["wall"] = clock.report()
     print(json.dumps(out), flush=True)
 
 
@@ -291,39 +455,95 @@ def combine_kernels(mvx):
 
 # ------------------------------------------------------------------ common --
 
-def timed(args, step, stream, world):
+class StepFailure(Exception):
+    """A block of steps returned an error (worst = 1) or did not complete in
+    time (worst = 2) on some rank; every rank raises it alike."""
+
+    def __init__(self, worst, limit):
+        super().__init__(worst)
+        self.worst, self.limit = worst, limit
+
+    def text(self):
+        return ("an error return on some rank" if self.worst == 1 else
+                "a step did not complete within %.0f s" % self.limit)
+
+
+def timed(args, step, stream, world, agree=None, limit=None):
     """W untimed steps, then K steps between barrier + synchronize, with one
     HIP event pair on the launch stream around them (the mean: nothing else
     is enqueued between the steps).  Then, untimed, K more steps with an
     event after each for the median / min (an event between two kernels adds
-    a few microseconds of its own, so these are not used for the mean)."""
+    a few microseconds of its own, so these are not used for the mean).
+
+    N > 1 (agree given): every block of steps ends in a bounded wait for the
+    launch stream (busy polling, `limit` seconds) and a status agreement over
+    gloo -- the barrier -- so an error return or a step that never completes
+    on any rank raises StepFailure on every rank instead of blocking them in
+    torch.cuda.synchronize or killing one rank."""
     import torch
     import torch.distributed as dist
 
-    def barrier():
+    def settle(block):
+        if agree is None:
+            block()
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            return
+        st = 0
+        try:
+            block()
+        except RuntimeError:
+            st = 1
+        if st == 0 and not _wait_stream(stream, limit, spin=True):
+            st = 2
+        worst = agree(st)
+        if worst:
+            raise StepFailure(worst, limit)
         torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
 
-    for _ in range(args.warmup):
-        step()
-    barrier()
+    def run(k, evs=None):
+        def block():
+            for i in range(k):
+                step()
+                if evs is not None:
+                    evs[i + 1].record(stream)
+        return block
+
+    settle(run(args.warmup))
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    e0.record(stream)
-    for i in range(args.steps):
-        step()
-    e1.record(stream)
-    torch.cuda.synchronize()
-    wall = time.perf_counter() - t0      # this rank's K steps; MAX over ranks below
-    barrier()
+    wall = [0.0]
+
+    def timed_block():
+        t0 = time.perf_counter()
+        e0.record(stream)
+        run(args.steps)()
+        e1.record(stream)
+        if agree is None:
+            torch.cuda.synchronize()
+        elif not _wait_stream(stream, limit, spin=True):
+            raise _Hung()
+        wall[0] = time.perf_counter() - t0      # this rank's K steps; MAX over ranks below
+
+    if agree is None:
+        timed_block()
+        settle(lambda: None)
+    else:
+        st = 0
+        try:
+            timed_block()
+        except RuntimeError:
+            st = 1
+        except _Hung:
+            st = 2
+        worst = agree(st)
+        if worst:
+            raise StepFailure(worst, limit)
+    wall = wall[0]
     dev_ms = e0.elapsed_time(e1)
     evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     evs[0].record(stream)
-    for i in range(args.steps):
-        step()
-        evs[i + 1].record(stream)
-    barrier()
+    settle(run(args.steps, evs))
     per = [evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)]
     t_local = max(wall, dev_ms / 1e3)
     if world > 1:
@@ -401,19 +621,30 @@ def plan_bytes(mvx, coll, world, rank, n, cnts, dtype, op):
     return out
 
 
-def phase_breakdown(comm, step, coll, world, nbytes, pb, reps=3):
+def phase_breakdown(comm, step, coll, world, nbytes, pb, stream, agree, limit, reps=3):
     """Untimed, after the timed region: `reps` more steps with HIP events
     around phase A (exchange), B (combine) and C (distribution) on the launch
     stream (mvx_comm_set_phase_timing); the median of each, MAX over ranks,
     with the rate each phase reached: A / C as the bytes each rank sends and
     receives per ms (and per link: the largest single peer's share over the
-    phase time, against XGMI_LINK_GBS), B as the combine's HBM bytes."""
+    phase time, against XGMI_LINK_GBS), B as the combine's HBM bytes.  Each
+    step is waited for with a bound (StepFailure, as in timed())."""
     import torch
     import torch.distributed as dist
     comm.set_phase_timing(True)
     got = []
     for _ in range(reps):
-        step()
+        st = 0
+        try:
+            step()
+        except RuntimeError:
+            st = 1
+        if st == 0 and not _wait_stream(stream, limit):
+            st = 2
+        worst = agree(st)
+        if worst:
+            comm.set_phase_timing(False)
+            raise StepFailure(worst, limit)
         got.append(comm.phase_times())
     comm.set_phase_timing(False)
     out = {}
@@ -457,13 +688,20 @@ def _hang_injected(name, rank):
     return any(x == "%s@%d" % (name, rank) for x in spec.split(",") if x)
 
 
-def _wait_stream(stream, seconds):
-    """True once the stream drained, False after `seconds` (a hung transfer)"""
+class _Hung(Exception):
+    pass
+
+
+def _wait_stream(stream, seconds, spin=False):
+    """True once the stream drained, False after `seconds` (a hung transfer).
+    spin: poll without sleeping (inside a timed region, where a 0.5 ms nap
+    would be read as step time)."""
     t0 = time.perf_counter()
+    nap = 0.0 if spin else 0.0005
     while not stream.query():
         if time.perf_counter() - t0 > seconds:
             return False
-        time.sleep(0.0005)
+        time.sleep(nap)
     return True
 
 
@@ -484,11 +722,29 @@ def choose_variant(names, tried):
 EXTRA_AT = {4: ["c4"], 8: ["c5"]}
 
 
+def step_limit(args, est_s):
+    """Seconds a block of steps may take before it counts as hung: the
+    variant timeout, or 10 x the block at the checked step's pace."""
+    return max(args.variant_timeout, 10.0 * max(args.steps, args.warmup, 1) * est_s)
+
+
+def checked_step(step, stream, limit):
+    """One step and a bounded wait: (status 0 ok / 1 error / 2 hung, seconds)"""
+    t0 = time.perf_counter()
+    try:
+        step()
+    except RuntimeError:
+        return 1, time.perf_counter() - t0
+    ok = _wait_stream(stream, limit)
+    return (0 if ok else 2), time.perf_counter() - t0
+
+
 def run_extra(args, mvx, dev, world, rank, comm, exch_name, cfg, agree, stream):
     """After the line is measured: one more BASELINE config on the same
     communicator -- its reference digests (rank 0, the reference schedule on
     p host threads, untimed), one checked step (a hang or an error is
-    recorded, not fatal), then W + K timed steps.  Returns a summary dict."""
+    recorded, not fatal), then W + K timed steps.  Returns (summary, worst
+    status: 0 ok, 1 error, 2 hung)."""
     import torch
     import torch.distributed as dist
     coll, dtype, op, E, mib, desc = CONFIGS[cfg]
@@ -519,11 +775,7 @@ def run_extra(args, mvx, dev, world, rank, comm, exch_name, cfg, agree, stream):
         if rc:
             raise RuntimeError("%s rc=%d" % (coll, rc))
 
-    try:
-        step()
-        status = 0 if _wait_stream(stream, args.variant_timeout) else 2
-    except RuntimeError:
-        status = 1
+    status, est = checked_step(step, stream, args.variant_timeout)
     worst = agree(status)
     if worst:
         out["error"] = "an error return on some rank" if worst == 1 else "the checked step did not complete"
@@ -534,7 +786,11 @@ def run_extra(args, mvx, dev, world, rank, comm, exch_name, cfg, agree, stream):
         dist.all_gather_object(allg, _digest(recvbuf.cpu().numpy()))
         parity = allg == ref
     out["exchange_ran"] = EXCH_NAMES.get(comm.last_exchange(), "?")
-    times = timed(args, step, stream, world)
+    try:
+        times = timed(args, step, stream, world, agree, step_limit(args, est))
+    except StepFailure as e:
+        out["error"] = "timed steps: " + e.text()
+        return out, e.worst
     p = world
     sec = times["t_job"] / args.steps
     busbw = (2 if coll == "allreduce" else 1) * (p - 1) / p * nbytes / sec / 1e9
@@ -569,11 +825,7 @@ def rccl_native(args, mvx, comm, cfg, n, sendbuf, world, dev, stream, agree, lin
         if rc:
             raise RuntimeError("mvx_comm_rccl_native rc=%d" % rc)
 
-    try:
-        step()
-        status = 0 if _wait_stream(stream, args.variant_timeout) else 2
-    except RuntimeError:
-        status = 1
+    status, est = checked_step(step, stream, args.variant_timeout)
     worst = agree(status)
     res = {"op": "ncclAllReduce(ncclSum)" if coll == "allreduce" else "ncclReduceScatter(ncclSum)",
            "note": "RCCL's own reduction on the same communicator and vectors (SURVEY.md 8(e) ablation): "
@@ -582,7 +834,11 @@ def rccl_native(args, mvx, comm, cfg, n, sendbuf, world, dev, stream, agree, lin
     if worst:
         res["error"] = "an error return on some rank" if worst == 1 else "the checked step did not complete"
         return res, worst
-    times = timed(args, step, stream, world)
+    try:
+        times = timed(args, step, stream, world, agree, step_limit(args, est))
+    except StepFailure as e:
+        res["error"] = "timed steps: " + e.text()
+        return res, e.worst
     sec = times["t_job"] / args.steps
     p = world
     nbytes = n * E
@@ -594,7 +850,36 @@ def rccl_native(args, mvx, comm, cfg, n, sendbuf, world, dev, stream, agree, lin
     return res, 0
 
 
-def run_multi(args, mvx, dev, world, rank, local):
+def rccl_view(comm, world, dev, transport):
+    """RCCL's own account of the communicator, every rank's answer
+    all-gathered (mvx_comm_rccl_info: ncclCommCount, ncclCommCuDevice,
+    ncclGetVersion) next to the HIP device each rank drives (PCI location,
+    UUID): what says the N ranks of the line sat on N distinct GPUs."""
+    import torch
+    import torch.distributed as dist
+    info = comm.rccl_info()
+    pr = torch.cuda.get_device_properties(dev)
+    me = {"rccl": info, "hip_device": dev.index,
+          "pci": "%04x:%02x:%02x" % (pr.pci_domain_id, pr.pci_bus_id, pr.pci_device_id),
+          "uuid": str(getattr(pr, "uuid", ""))}
+    allg = [None] * world
+    dist.all_gather_object(allg, me)
+    out = {"transport": transport,
+           "hip_devices": [a["hip_device"] for a in allg],
+           "pci": [a["pci"] for a in allg],
+           "distinct_gpus": len({a["uuid"] or a["pci"] for a in allg})}
+    if any(a["rccl"] is None for a in allg):
+        out.update(nranks=None, devices=None, version=None,
+                   note="no RCCL communicator (caller-supplied transport)")
+        return out
+    nr = [a["rccl"]["nranks"] for a in allg]
+    out.update(nranks=nr[0] if len(set(nr)) == 1 else nr,
+               devices=[a["rccl"]["device"] for a in allg],
+               version=allg[0]["rccl"]["version"])
+    return out
+
+
+def run_multi(args, mvx, dev, world, rank, local, clock):
     import torch
     import torch.distributed as dist
     cfg = args.config or "c3"
@@ -612,14 +897,18 @@ def run_multi(args, mvx, dev, world, rank, local):
         return mvx.Comm.from_torch_distributed(dev.index)
 
     comm = new_comm()
+    rccl = rccl_view(comm, world, dev, args.transport)
+    clock.mark("communicator")
     sets = max(1, min(args.sets, 2))
     sendbuf = [synth(cfg, n, rank, dev) for _ in range(sets)]
     nrecv = n // world if coll == "reduce_scatter" else n
     recvbuf = [torch.empty(nrecv * E, dtype=torch.uint8, device=dev) for _ in range(sets)]
     cnts = [n // world] * world
     comm.reserve(2 * nbytes)
+    torch.cuda.synchronize()
+    clock.mark("inputs")
     it = [0]
-    cur = {"name": None, "comm": comm}
+    cur = {"name": None, "comm": comm, "best": None}
 
     def step():
         s = it[0] % sets
@@ -651,6 +940,7 @@ def run_multi(args, mvx, dev, world, rank, local):
         box = [ref]
         dist.broadcast_object_list(box, src=0)
         ref = box[0]
+    clock.mark("reference run (rank 0)")
 
     def agree(flag):
         """every rank's status, MAX over ranks (gloo: the host side, which a
@@ -658,16 +948,6 @@ def run_multi(args, mvx, dev, world, rank, local):
         t = torch.tensor([flag], dtype=torch.int64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return int(t.item())
-
-    def trial():
-        """one untimed step of the current variant on set 0: 0 ok, 1 an
-        error return, 2 the step never completed"""
-        it[0] = 0
-        try:
-            step()
-        except RuntimeError:
-            return 1
-        return 0 if _wait_stream(stream, args.variant_timeout) else 2
 
     def parity_check():
         """set 0's result on every rank against the reference's digests"""
@@ -678,15 +958,49 @@ def run_multi(args, mvx, dev, world, rank, local):
         dist.all_gather_object(allg, mine)
         return allg == ref
 
-    def measure(name):
+    def emit(out):
+        """rank 0 prints the line, with where the wall clock went"""
+        if rank == 0 and out is not None:
+            out["config"]["exchange_tuning"] = tried
+            out["rccl"] = rccl
+            out["env"] = env_echo()
+            clock.mark("finish")
+            out["wall"] = clock.report()
+            print(json.dumps(out), flush=True)
+
+    def recover(worst, entry):
+        """after a failed block on every rank: a hang tears the communicator
+        down (ncclCommAbort) and builds a fresh one.  If the stream stays
+        blocked even then, rank 0 prints the line already measured and the
+        run ends (exit 0 with a line, 1 without)."""
+        if worst != 2:
+            return
+        cur["comm"].abort()
+        if agree(0 if _wait_stream(stream, args.variant_timeout) else 1):
+            entry["error"] += "; the stream stayed blocked after ncclCommAbort"
+            emit(cur["best"])
+            sys.stdout.flush()
+            sys.stderr.flush()
+            os._exit(0 if cur["best"] is not None else 1)
+        cur["comm"] = new_comm()
+        cur["comm"].reserve(2 * nbytes)
+
+    def measure(name, est_s):
         """the K timed steps (and the per-phase breakdown) of variant `name`:
-        one candidate line"""
+        one candidate line.  StepFailure propagates from the timed steps; a
+        failure in the untimed phase steps is recorded in the line's phases
+        and returned as its status."""
         cur["name"] = name
         cur["comm"].set_exchange(*EXCH[name])
-        times = timed(args, step, stream, world)
+        limit = step_limit(args, est_s)
+        times = timed(args, step, stream, world, agree, limit)
         ran = EXCH_NAMES.get(cur["comm"].last_exchange(), "?")
         pb = plan_bytes(mvx, coll, world, rank, n, cnts, dtype, op)
-        phases = phase_breakdown(cur["comm"], step, coll, world, nbytes, pb)
+        status = 0
+        try:
+            phases = phase_breakdown(cur["comm"], step, coll, world, nbytes, pb, stream, agree, limit)
+        except StepFailure as e:
+            phases, status = {"error": "phase-timing steps: " + e.text()}, e.worst
         p = world
         sec = times["t_job"] / args.steps
         if coll == "allreduce":
@@ -711,32 +1025,29 @@ def run_multi(args, mvx, dev, world, rank, local):
         out["parity"] = (("bit-exact vs the reference schedule, all %d ranks" % p) if parity
                          else ("MISMATCH" if parity is False else None))
         out["cpu_baseline"] = cpu
-        return out
+        return out, status
 
     # Exchange variants in EXCH order (p2p first, coll last).  Each gets one
     # checked step, then --tune-steps timed steps if every rank completed it
-    # without an error; a variant that errs or never completes on any rank is
-    # recorded and left out (a hung one first tears the communicator down and
-    # builds a fresh one).  The first clean variant is measured for the line
-    # at once (K timed steps), and a later one is measured again only if its
-    # tuning steps ran faster -- so a line exists before any riskier variant
-    # runs, and a variant that wedges the GPU for good ends the run with the
-    # line already measured rather than with none.
+    # without an error; a variant that errs or never completes on any rank --
+    # in its checked step, its tuning steps, its timed steps or its phase
+    # steps -- is recorded and left out (a hung one first tears the
+    # communicator down and builds a fresh one).  The first clean variant is
+    # measured for the line at once (K timed steps), and a later one is
+    # measured again only if its tuning steps ran faster -- so a line exists
+    # before any riskier variant runs, and a variant that wedges the GPU for
+    # good ends the run with the line already measured rather than with none.
     names = list(EXCH) if args.exchange == "auto" else [args.exchange]
     tried = {}
-    best = None
-
-    def finish(out):
-        if out is not None:
-            out["config"]["exchange_tuning"] = tried
-        return out
 
     for name in names:
         mode, slices = EXCH[name]
         cur["name"] = name
         status = 1 if cur["comm"].set_exchange(mode, slices) else 0
+        est = 0.0
         if agree(status) == 0:
-            status = trial()
+            it[0] = 0
+            status, est = checked_step(step, stream, args.variant_timeout)
         worst = agree(status)
         ok, ran = None, None
         if worst == 0:
@@ -745,22 +1056,13 @@ def run_multi(args, mvx, dev, world, rank, local):
             if ran != EXCH_NAMES[mode]:
                 ran += " (fallback)"
         entry = {"ran": ran}
+        tried[name] = entry
         if worst:
             entry.update(ms_per_step=None, parity=None,
                          error="an error return on some rank" if worst == 1 else
                                "a step did not complete within %.0f s" % args.variant_timeout)
-            tried[name] = entry
-            if worst == 2:
-                cur["comm"].abort()
-                if agree(0 if _wait_stream(stream, args.variant_timeout) else 1):
-                    # still wedged after the abort: report what was measured
-                    entry["error"] += "; the stream stayed blocked after ncclCommAbort"
-                    if rank == 0 and best is not None:
-                        print(json.dumps(finish(best)), flush=True)
-                    sys.stdout.flush()
-                    os._exit(0 if best is not None else 1)
-                cur["comm"] = new_comm()
-                cur["comm"].reserve(2 * nbytes)
+            recover(worst, entry)
+            clock.mark("variant %s" % name)
             continue
         t = torch.zeros(1, dtype=torch.float64)
         torch.cuda.synchronize()
@@ -775,7 +1077,9 @@ def run_multi(args, mvx, dev, world, rank, local):
             except RuntimeError:
                 terr = 1
             issue.append(time.perf_counter() - t1)
-        torch.cuda.synchronize()
+        tlim = step_limit(args, est)
+        if terr == 0 and not _wait_stream(stream, tlim, spin=True):
+            terr = 2
         t[0] = time.perf_counter() - t0
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         # host time inside one collective call (plan, staging, RCCL enqueue
@@ -783,27 +1087,43 @@ def run_multi(args, mvx, dev, world, rank, local):
         # median over the tuning steps, MAX over ranks
         hi = torch.tensor([statistics.median(issue)], dtype=torch.float64)
         dist.all_reduce(hi, op=dist.ReduceOp.MAX)
-        if agree(terr):
-            entry.update(ms_per_step=None, parity=ok, error="an error return on some rank while tuning")
-        else:
-            entry.update(ms_per_step=round(float(t.item()) * 1e3 / args.tune_steps, 4), parity=ok,
-                         host_issue_us=round(float(hi.item()) * 1e6, 1))
-        tried[name] = entry
+        worst = agree(terr)
+        if worst:
+            entry.update(ms_per_step=None, parity=ok,
+                         error=("an error return on some rank while tuning" if worst == 1 else
+                                "a tuning step did not complete within %.0f s" % tlim))
+            recover(worst, entry)
+            clock.mark("variant %s" % name)
+            continue
+        torch.cuda.synchronize()
+        entry.update(ms_per_step=round(float(t.item()) * 1e3 / args.tune_steps, 4), parity=ok,
+                     host_issue_us=round(float(hi.item()) * 1e6, 1))
         # measure for the line: the first clean variant, then any that tuned
         # faster than the one measured (every rank decides alike: the tuning
         # time is the MAX over ranks and parity is compared on every rank)
+        best = cur["best"]
         if choose_variant([name], tried) == name and (
                 best is None or entry["ms_per_step"] < tried[best["config"]["exchange"]]["ms_per_step"]):
             box = [name]
             dist.broadcast_object_list(box, src=0)
-            cand = measure(box[0])
+            try:
+                cand, pstat = measure(box[0], max(est, entry["ms_per_step"] * 1e-3))
+            except StepFailure as e:
+                entry.update(ms_per_step=None, error="timed steps: " + e.text())
+                recover(e.worst, entry)
+                clock.mark("variant %s" % name)
+                continue
             if best is None or cand["ms_per_step"] < best["ms_per_step"]:
-                best = cand
-    if best is None:
+                cur["best"] = cand
+            if pstat:
+                entry["error"] = cand["roofline"]["phases"]["error"]
+                recover(pstat, entry)
+        clock.mark("variant %s" % name)
+    out = cur["best"]
+    if out is None:
         if rank == 0:
             sys.stderr.write("bench: no exchange variant ran clean with parity: %s\n" % json.dumps(tried))
-        return None
-    out = finish(best)
+        return None, emit
     # the other BASELINE configs quoted at this GPU count, on the same
     # communicator and exchange variant, after the line's timed region
     extras = EXTRA_AT.get(world, []) if args.extra_configs == "auto" else \
@@ -815,6 +1135,7 @@ def run_multi(args, mvx, dev, world, rank, local):
         res, worst = run_extra(args, mvx, dev, world, rank, cur["comm"], out["config"]["exchange"], cfg2,
                                agree, stream)
         others.append(res)
+        clock.mark("other config %s" % cfg2)
         if worst == 2:           # a hang: leave the communicator, keep the line
             cur["comm"].abort()
             aborted = True
@@ -826,22 +1147,31 @@ def run_multi(args, mvx, dev, world, rank, local):
                                  out["ms_per_step"])
         if nat is not None:
             out["rccl_native"] = nat
+            clock.mark("rccl native")
         if worst == 2:
             cur["comm"].abort()
             aborted = True
     if not aborted:
         cur["comm"].free()
-    return out
+    return out, emit
 
 
-def main():
-    args = parse()
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    how, val = decide_launch(args.gpus, os.environ)
+    if how == "mismatch":
+        sys.stderr.write("bench: %s\n" % val)
+        sys.exit(2)
+    if how == "self":
+        sys.exit(launch(args, val, argv))
+    world = val
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    clock = Stages(verbose=rank == 0 and world > 1)
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.transport == "rccl-net":
         importlib.import_module("mvapich-cce_amd.transport").rccl_net_env(rank)
     dev_index = local % torch.cuda.device_count() if args.transport != "rccl" else local
@@ -852,8 +1182,9 @@ def main():
         mvx.set_launch(args.block_cap, args.nt_min_log2)
     if world == 1:
         if args.config not in (None, "c2"):
-            sys.exit("configs c3-c5 are multi-GPU: run under torchrun with --nproc-per-node N")
-        run_single(args, mvx, dev)
+            sys.exit("configs c3-c5 are multi-GPU: run with --gpus N (N > 1)")
+        clock.mark("start-up (imports)")
+        run_single(args, mvx, dev, clock)
         return
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     # gloo bootstraps, agrees and checks (and is the host transport's byte
@@ -863,9 +1194,9 @@ def main():
     import datetime
     dist.init_process_group("gloo", rank=rank, world_size=world,
                             timeout=datetime.timedelta(seconds=args.gloo_timeout))
-    out = run_multi(args, mvx, dev, world, rank, local)
-    if rank == 0 and out is not None:
-        print(json.dumps(out), flush=True)
+    clock.mark("start-up (imports, process group)")
+    out, emit = run_multi(args, mvx, dev, world, rank, local, clock)
+    emit(out)
     dist.barrier()
     dist.destroy_process_group()
     if out is None:

@@ -112,6 +112,10 @@ int mvx_comm_abort(MPI_Comm *comm);
  * on a communicator without RCCL (virtual, caller transport). */
 int mvx_comm_rccl_native(MPI_Comm comm, int coll, const void *sendbuf, void *recvbuf, size_t count,
                          MPI_Datatype dt, void *stream);
+/* RCCL's own view of an RCCL communicator: ncclCommCount, ncclCommCuDevice
+ * (this rank's device) and ncclGetVersion; any pointer may be NULL.
+ * MPI_ERR_COMM on a communicator without RCCL (virtual, caller transport). */
+int mvx_comm_rccl_info(MPI_Comm comm, int *nranks, int *device, int *version);
 /* Per-phase timing (diagnostics): with timing on, each device-buffer call
  * records HIP events on its stream around phase A (exchange), B (combine)
  * and C (distribution).  mvx_comm_phase_times waits for the last timed call

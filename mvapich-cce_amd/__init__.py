@@ -138,6 +138,7 @@ def _load():
     c.mvx_comm_free.argtypes = [pi]
     c.mvx_comm_abort.argtypes = [pi]
     c.mvx_comm_rccl_native.argtypes = [i, i, vp, vp, sz, i, vp]
+    c.mvx_comm_rccl_info.argtypes = [i, pi, pi, pi]
     c.mvx_comm_set_stream.argtypes = [i, vp]
     c.mvx_comm_reserve.argtypes = [i, sz]
     c.mvx_comm_set_exchange.argtypes = [i, i, i]

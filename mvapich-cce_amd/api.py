@@ -173,6 +173,16 @@ class Comm:
         return coll().mvx_comm_rccl_native(self.handle, coll_kind, addr(sendbuf), addr(recvbuf), count, dtype,
                                            stream_handle(stream))
 
+    def rccl_info(self):
+        """RCCL's own view (mvx_comm_rccl_info): {nranks, device, version}
+        from ncclCommCount / ncclCommCuDevice / ncclGetVersion; None on a
+        communicator without RCCL."""
+        n, d, v = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        rc = coll().mvx_comm_rccl_info(self.handle, ctypes.byref(n), ctypes.byref(d), ctypes.byref(v))
+        if rc:
+            return None
+        return {"nranks": n.value, "device": d.value, "version": v.value}
+
     def reserve(self, nbytes):
         return coll().mvx_comm_reserve(self.handle, nbytes)
 

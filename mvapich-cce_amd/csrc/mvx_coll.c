@@ -411,6 +411,22 @@ int mvx_comm_rccl_native(MPI_Comm comm, int coll, const void *sendbuf, void *rec
     return r == ncclSuccess ? MPI_SUCCESS : MPI_ERR_OTHER;
 }
 
+/* What RCCL itself reports for the communicator: its rank count
+ * (ncclCommCount), the device it drives for this rank (ncclCommCuDevice)
+ * and its version (ncclGetVersion) -- bench.py puts every rank's answer in
+ * its line so "did RCCL see N ranks on N GPUs" is read off RCCL, not off
+ * the launcher's environment.  MPI_ERR_COMM without an RCCL handle. */
+int mvx_comm_rccl_info(MPI_Comm comm, int *nranks, int *device, int *version)
+{
+    mvx_comm_t *c = get_comm(comm);
+    if (!c) return ERR_COMM_NULL_CODE;
+    if (c->local || c->has_ops || !c->nccl) return MPI_ERR_COMM;
+    if (nranks && ncclCommCount(c->nccl, nranks) != ncclSuccess) return MPI_ERR_OTHER;
+    if (device && ncclCommCuDevice(c->nccl, device) != ncclSuccess) return MPI_ERR_OTHER;
+    if (version && ncclGetVersion(version) != ncclSuccess) return MPI_ERR_OTHER;
+    return MPI_SUCCESS;
+}
+
 /* ---- per-phase timing of device calls -----------------------------------
  * With timing on, every device-buffer call records four events on its
  * stream: before phase A, after A, after B, after C (the pipelined variant,

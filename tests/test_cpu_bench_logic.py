@@ -56,3 +56,66 @@ def test_rccl_net_env_gives_each_rank_its_own_host():
     assert len({e["NCCL_HOSTID"] for e in envs}) == 8
     assert all(e["NCCL_SOCKET_IFNAME"] == "lo" and e["NCCL_IB_DISABLE"] == "1" for e in envs)
     assert tp.rccl_net_env(3, {"NCCL_SOCKET_IFNAME": "eth0"})["NCCL_SOCKET_IFNAME"] == "eth0"
+
+
+def test_launch_decision():
+    """--gpus N without a launcher starts N workers itself; under a launcher
+    --gpus must name the launcher's world size (or be absent)."""
+    assert bench.decide_launch(None, {}) == ("single", 1)
+    assert bench.decide_launch(1, {}) == ("single", 1)
+    assert bench.decide_launch(8, {}) == ("self", 8)
+    assert bench.decide_launch(8, {"WORLD_SIZE": "8"}) == ("worker", 8)
+    assert bench.decide_launch(None, {"WORLD_SIZE": "4"}) == ("worker", 4)
+    assert bench.decide_launch(1, {"WORLD_SIZE": "1"}) == ("single", 1)
+    how, msg = bench.decide_launch(8, {"WORLD_SIZE": "2"})
+    assert how == "mismatch" and "WORLD_SIZE=2" in msg
+    assert bench.decide_launch(0, {})[0] == "mismatch"
+
+
+def test_worker_env_is_torchrun_shaped():
+    env = bench.worker_env({"PATH": "/bin", "HSA_ENABLE_IPC_MODE_LEGACY": "0"}, 3, 8, 29500)
+    assert env["RANK"] == env["LOCAL_RANK"] == "3"
+    assert env["WORLD_SIZE"] == env["LOCAL_WORLD_SIZE"] == "8"
+    assert env["MASTER_ADDR"] == "127.0.0.1" and env["MASTER_PORT"] == "29500"
+    assert env["HSA_ENABLE_IPC_MODE_LEGACY"] == "0" and env["PATH"] == "/bin"
+    assert bench.decide_launch(8, env) == ("worker", 8)
+    assert bench._rc_of(0) == 0 and bench._rc_of(1) == 1 and bench._rc_of(-9) == 137
+
+
+def test_mismatched_world_exits_nonzero_before_any_gpu_work():
+    """WORLD_SIZE from a launcher that disagrees with --gpus: exit 2 at once
+    (main() returns before importing torch)."""
+    import subprocess
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4"], env=env,
+                       capture_output=True, text=True, timeout=60)
+    assert p.returncode == 2, (p.returncode, p.stderr)
+    assert "WORLD_SIZE=2" in p.stderr and not p.stdout.strip()
+
+
+def test_self_launch_refuses_more_rccl_ranks_than_gpus():
+    """Without a GPU (this container) --gpus 2 over RCCL cannot place its
+    ranks: the launcher says so and exits 2 before starting workers."""
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["HIP_VISIBLE_DEVICES"] = env.get("HIP_VISIBLE_DEVICES", "")
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert p.returncode == 2, (p.returncode, p.stderr[-2000:])
+    assert "needs 2 GPUs" in p.stderr
+
+
+def test_stages_partition_the_wall_clock():
+    st = bench.Stages()
+    st.mark("a")
+    st.mark("b")
+    st.mark("a")
+    r = st.report()
+    assert set(r["stage_s"]) == {"a", "b"}
+    assert abs(sum(r["stage_s"].values()) + r["unaccounted_s"] - r["wall_s"]) < 0.01
+
+
+def test_env_echo_keeps_only_the_knobs():
+    e = bench.env_echo({"NCCL_DEBUG": "INFO", "HOME": "/root", "MVX_EXCHANGE": "coll", "RCCL_X": "1",
+                        "HSA_ENABLE_IPC_MODE_LEGACY": "0"})
+    assert e == {"HSA_ENABLE_IPC_MODE_LEGACY": "0", "MVX_EXCHANGE": "coll", "NCCL_DEBUG": "INFO", "RCCL_X": "1"}

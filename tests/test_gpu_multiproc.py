@@ -290,3 +290,65 @@ def test_bench_line_carries_the_other_baseline_configs():
     (o,) = d["other_configs"]
     assert o["config"] == "c4" and o["parity"].startswith("bit-exact"), o
     assert o["value"] > 0 and o["busbw_GBs"] > 0 and o["exchange"] == d["config"]["exchange"]
+
+
+def _bench_self(world, transport, extra=(), extra_env=None):
+    """bench.py in the driver's own form -- no torchrun, no WORLD_SIZE:
+    --gpus N starts its N workers itself (bench.launch)."""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_PORT")}
+    env["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
+    env.update(extra_env or {})
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--steps", "2", "--warmup", "1",
+           "--tune-steps", "1", "--mib", "16", "--transport", transport] + list(extra)
+    return subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=400)
+
+
+def _one_line(p):
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = [x for x in p.stdout.splitlines() if x.startswith("{")]
+    assert len(line) == 1, p.stdout[-2000:]
+    return json.loads(line[0])
+
+
+@pytest.mark.parametrize("transport", ["host", "rccl-net"])
+def test_bench_self_launch_driver_form(transport):
+    """`python3 bench.py --gpus 2 ...` with no launcher prints ONE 2-rank
+    line: n_gpus 2, parity bit-exact on both ranks, the launcher's record,
+    RCCL's own rank count (rccl-net: ncclCommCount = 2, one device per rank),
+    the env knobs echoed, and per-stage wall times that add up to the run's
+    wall clock."""
+    d = _one_line(_bench_self(2, transport))
+    assert d["n_gpus"] == 2 and d["value"] > 0
+    assert d["parity"] == "bit-exact vs the reference schedule, all 2 ranks", d["parity"]
+    assert d["launch"]["workers"] == 2 and d["launch"]["worker_rcs"] == [0, 0], d["launch"]
+    r = d["rccl"]
+    assert r["transport"] == transport and len(r["hip_devices"]) == 2
+    if transport == "rccl-net":
+        assert r["nranks"] == 2 and len(r["devices"]) == 2 and r["version"] > 0, r
+    else:
+        assert r["nranks"] is None, r
+    assert d["env"].get("HSA_ENABLE_IPC_MODE_LEGACY") == "0"
+    w = d["wall"]
+    total = sum(w["stage_s"].values()) + w["unaccounted_s"]
+    assert abs(total - w["wall_s"]) <= 0.05 * w["wall_s"], w
+    assert w["wall_s"] <= d["launch"]["wall_s"] + 1.0, (w, d["launch"])
+    assert any(k.startswith("variant ") for k in w["stage_s"]), w
+
+
+def test_bench_self_launch_worker_failure_exits_nonzero():
+    """Workers that end without a line take the job down: the launcher exits
+    with their worst code and prints no line (every variant fails on rank 1)."""
+    p = _bench_self(2, "host", extra_env={"MVX_BENCH_FAIL": ",".join(
+        "%s@1" % v for v in ("p2p", "pipe", "pipe2", "pipe8", "coll"))})
+    assert p.returncode != 0
+    assert not [x for x in p.stdout.splitlines() if x.startswith("{")]
+
+
+def test_bench_self_launch_rccl_xgmi():
+    """The same over RCCL proper when the box has 2 GPUs (on the node: xGMI)."""
+    if _ngpus() < 2:
+        pytest.skip("needs 2 GPUs")
+    d = _one_line(_bench_self(2, "rccl"))
+    assert d["n_gpus"] == 2 and d["rccl"]["nranks"] == 2 and d["rccl"]["distinct_gpus"] == 2, d["rccl"]
+    assert d["parity"].startswith("bit-exact"), d
