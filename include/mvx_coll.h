@@ -63,8 +63,18 @@ typedef struct mvx_transport {
     int (*alltoall)(void *ctx, const void *sendbuf, void *recvbuf, size_t bytes, void *stream);
     int (*allgather)(void *ctx, void *buf, size_t bytes, void *stream);
 } mvx_transport;
+/* The table's base (ctx and the four phase callbacks): what every caller
+ * has, whichever header it was compiled against. */
+#define MVX_TRANSPORT_BASE_BYTES offsetof(mvx_transport, alltoall)
+/* Reads the table's base only: a transport given here has no collective
+ * hooks (MVX_EXCH_COLL runs as P2P). */
 int mvx_comm_init_transport(MPI_Comm *comm, int rank, int size, int device,
                             const mvx_transport *transport);
+/* Reads the first `bytes` of the table (pass sizeof(mvx_transport)): the
+ * hooks when the caller's table has them, none when it is shorter.
+ * MPI_ERR_ARG below MVX_TRANSPORT_BASE_BYTES. */
+int mvx_comm_init_transport_ex(MPI_Comm *comm, int rank, int size, int device,
+                               const mvx_transport *transport, size_t bytes);
 /* helpers for transports: a blocking copy between any two pointers
  * (hipMemcpyDefault) and a stream synchronisation */
 int mvx_copy(void *dst, const void *src, size_t bytes);
@@ -102,6 +112,18 @@ int mvx_comm_last_exchange(MPI_Comm comm, int *mode);
  * handle is freed as by mvx_comm_free; the staging memory is not (work
  * queued behind the aborted transfers may still read it). */
 int mvx_comm_abort(MPI_Comm *comm);
+/* Frees the staging of aborted communicators whose queued work has drained
+ * (an event recorded behind it on every stream they used has completed);
+ * runs at every communicator creation and mvx_comm_reserve too.  Returns
+ * how many aborted communicators' staging is still held. */
+int mvx_comm_reap(void);
+/* Host buffers at p > 1 on a one-rank-per-process communicator.  Default
+ * (0): the call copies them into HBM mirrors and moves exactly what a
+ * device-buffer call moves, so ranks may pass different buffer kinds in
+ * one call, as MPI allows.  1: the sliced pipeline (H2D, collective and D2H
+ * of successive slices overlap; faster) -- every rank must then pass host
+ * buffers in every call.  Env at creation: MVX_HOST_PIPELINE=1. */
+int mvx_comm_set_host_pipeline(MPI_Comm comm, int on);
 /* Ablation only: RCCL's own ncclAllReduce (coll =
  * MVX_COLL_ALLREDUCE, count elements) or ncclReduceScatter (coll =
  * MVX_COLL_REDUCE_SCATTER, count elements per rank) with ncclSum on the
@@ -195,6 +217,21 @@ int mvx_coll_scan(void *sendbuf, void *recvbuf, int count, MPI_Datatype datatype
                   MPI_Op op, MPI_Comm comm);
 /* 1 if p is device (or managed) memory the device path can use directly */
 int mvx_buffer_is_device(const void *p);
+
+/* Registration cache for pageable host buffers (MVAPICH's dreg,
+ * mpid/ch_gen2/dreg.c:774-832): with it on, a pageable range a call uses is
+ * page-locked (hipHostRegister) on first use and kept, so later calls DMA
+ * it directly.  Off by default; MVX_HOST_REGISTER=1 turns it on,
+ * MVX_HOST_REGISTER_MAX_MIB (16384) caps the registered bytes (least
+ * recently used entries are dropped), MVX_HOST_REGISTER_MIN_KIB (1024) is
+ * the smallest range registered.  Contract: call mvx_host_unregister(addr)
+ * for a registered buffer before freeing it (the reference's mem_hooks.c
+ * does this from malloc hooks).  max_bytes 0 keeps the current cap; turning
+ * the cache off drops every registration. */
+int mvx_host_register_enable(int on, size_t max_bytes);
+/* Drops every registration containing addr: 0, or MPI_ERR_ARG if none. */
+int mvx_host_unregister(const void *addr);
+int mvx_host_register_stats(long *entries, size_t *bytes, long *hits, long *misses);
 
 int PMPI_Reduce(void *, void *, int, MPI_Datatype, MPI_Op, int, MPI_Comm);
 int PMPI_Allreduce(void *, void *, int, MPI_Datatype, MPI_Op, MPI_Comm);

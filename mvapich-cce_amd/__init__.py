@@ -133,6 +133,13 @@ def _load():
     c.mvx_comm_init.argtypes = [pi, i, i, i, vp]
     c.mvx_comm_init_local.argtypes = [pi, i, i]
     c.mvx_comm_init_transport.argtypes = [pi, i, i, i, vp]
+    c.mvx_comm_init_transport_ex.argtypes = [pi, i, i, i, vp, sz]
+    c.mvx_comm_set_host_pipeline.argtypes = [i, i]
+    c.mvx_comm_reap.argtypes = []
+    c.mvx_host_register_enable.argtypes = [i, sz]
+    c.mvx_host_unregister.argtypes = [vp]
+    c.mvx_host_register_stats.argtypes = [ctypes.POINTER(ctypes.c_long), ctypes.POINTER(ctypes.c_size_t),
+                                          ctypes.POINTER(ctypes.c_long), ctypes.POINTER(ctypes.c_long)]
     c.mvx_copy.argtypes = [vp, vp, sz]
     c.mvx_stream_synchronize.argtypes = [vp]
     c.mvx_comm_free.argtypes = [pi]

@@ -13,7 +13,7 @@ __all__ = [
     "addr", "stream_handle", "op_apply", "op_combine", "op_program", "Comm",
     "MPI_Allreduce", "MPI_Reduce", "MPI_Reduce_scatter", "MPI_Scan", "MPI_Op_create", "MPI_Op_free", "op_create_device",
     "MPIR_call", "op_errno", "last_kernel", "last_kernel_symbol", "last_launch", "set_launch",
-    "set_fortran_logical",
+    "set_fortran_logical", "comm_reap", "host_register_enable", "host_unregister", "host_register_stats",
     "MPI_Type_contiguous", "MPI_Type_commit", "MPI_Type_free", "MPI_Type_extent", "MPI_Type_size",
     "MPI_Type_vector", "MPI_Type_hvector", "MPI_Type_indexed", "MPI_Type_hindexed", "MPI_Type_struct",
     "MPI_Type_lb", "MPI_Type_ub", "type_layout", "type_set_handle", "type_pack", "type_unpack",
@@ -137,7 +137,9 @@ class Comm:
         if device is None:
             device = torch.cuda.current_device()
         h = ctypes.c_int()
-        rc = coll().mvx_comm_init_transport(ctypes.byref(h), rank, size, device, ctypes.byref(transport.struct()))
+        t = transport.struct()
+        rc = coll().mvx_comm_init_transport_ex(ctypes.byref(h), rank, size, device, ctypes.byref(t),
+                                               ctypes.sizeof(t))
         if rc:
             raise RuntimeError("mvx_comm_init_transport rc=%d" % rc)
         c = cls(h.value, rank, size, False)
@@ -162,6 +164,11 @@ class Comm:
         transfers (ncclCommAbort)."""
         h = ctypes.c_int(self.handle)
         return coll().mvx_comm_abort(ctypes.byref(h))
+
+    def set_host_pipeline(self, on=True):
+        """Host buffers at p > 1 through the sliced pipeline (every rank must
+        then pass host buffers) instead of HBM mirrors (mvx_comm_set_host_pipeline)."""
+        return coll().mvx_comm_set_host_pipeline(self.handle, 1 if on else 0)
 
     def set_stream(self, stream=None):
         return coll().mvx_comm_set_stream(self.handle, stream_handle(stream))
@@ -453,3 +460,27 @@ def MPIR_call(name, invec, inoutvec, length, datatype):
 
 def op_errno():
     return coll().mvx_op_errno()
+
+
+def comm_reap():
+    """mvx_comm_reap: free drained aborted communicators' staging; returns
+    how many are still held."""
+    return coll().mvx_comm_reap()
+
+
+def host_register_enable(on=True, max_bytes=0):
+    """The pageable-buffer registration cache (mvx_host_register_enable)."""
+    return coll().mvx_host_register_enable(1 if on else 0, max_bytes)
+
+
+def host_unregister(buf):
+    """mvx_host_unregister: drop the registrations containing buf's address
+    (call before freeing a registered buffer)."""
+    return coll().mvx_host_unregister(addr(buf))
+
+
+def host_register_stats():
+    """{entries, bytes, hits, misses} of the registration cache."""
+    e, b, h, m = ctypes.c_long(), ctypes.c_size_t(), ctypes.c_long(), ctypes.c_long()
+    coll().mvx_host_register_stats(ctypes.byref(e), ctypes.byref(b), ctypes.byref(h), ctypes.byref(m))
+    return {"entries": e.value, "bytes": b.value, "hits": h.value, "misses": m.value}

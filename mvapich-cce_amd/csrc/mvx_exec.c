@@ -1,0 +1,411 @@
+/*
+ * mvx_exec.c -- one rank's plan on device buffers (the fast path): phase A
+ * moves shards to the rank that combines them, phase B runs the combine
+ * program, phase C sends combined blocks where they are needed.  Three
+ * exchange variants drive the links (MVX_EXCH_*, include/mvx_coll.h); all
+ * compute the same bits.  Reference schedules: intra_Allreduce /
+ * intra_Reduce / intra_Reduce_scatter (intra_fns_new.c), as planned by
+ * mvx_plan.c.
+ */
+#include <string.h>
+
+#include "mvx_internal.h"
+
+/* ---- one rank's execution of its plan ---------------------------------- */
+
+/* staging layout: one slot per received shard, plus the temporary result
+ * of a non-root Reduce; returns the bytes this rank needs (slots are
+ * SLOT_STAGGER apart beyond their size). */
+static size_t exec_layout(rank_exec_t *X)
+{
+    const mvx_plan *P = X->P;
+    const long E = P->esize;
+    const char *like = X->sendbuf + P->c_src_off * E;
+    size_t need = 0;
+    int s;
+    for (s = 0; s < P->p; s++) {
+        X->slot[s] = 0;
+        if (P->a_recv[s].cnt) {
+            X->slot[s] = slot_at(need, like);
+            need = X->slot[s] + P->a_recv[s].cnt * E + SLOT_STAGGER;
+        }
+    }
+    X->tmp_off = 0;
+    if (P->c_dst_tmp) { X->tmp_off = slot_at(need, like); need = X->tmp_off + P->c_cnt * E; }
+    X->wide_n = P->has_combine ? mvxi_wide_temps(P) : 0;
+    X->wide_off = X->wide_slot = 0;
+    if (X->wide_n) {
+        X->wide_off = slot_at(need, like);
+        X->wide_slot = ((size_t)(P->c_cnt * E) + SLOT_STAGGER + 255) & ~(size_t)255;
+        need = X->wide_off + X->wide_slot * (size_t)X->wide_n;
+    }
+    return need;
+}
+
+static char *exec_out(const rank_exec_t *X)
+{
+    const mvx_plan *P = X->P;
+    return P->c_dst_tmp ? X->pool + X->tmp_off : X->recvbuf + P->c_dst_off * P->esize;
+}
+
+/* phase A: shards to the rank that combines them */
+static int exec_phase_a(rank_exec_t *X, mvx_xport *t, hipStream_t st)
+{
+    const mvx_plan *P = X->P;
+    const long E = P->esize;
+    int s, any = 0, rc = 0, rc2;
+    for (s = 0; s < P->p; s++) any |= (P->a_send[s].cnt || P->a_recv[s].cnt);
+    if (!any) return MPI_SUCCESS;
+    if ((rc = t->start(t))) return rc;
+    for (s = 0; s < P->p && !rc; s++) {
+        if (P->a_send[s].cnt)
+            rc = t->send(t, X->sendbuf + P->a_send[s].off * E, (size_t)(P->a_send[s].cnt * E), s, st);
+        if (!rc && P->a_recv[s].cnt)
+            rc = t->recv(t, X->pool + X->slot[s], (size_t)(P->a_recv[s].cnt * E), s, st);
+    }
+    rc2 = t->end(t);
+    return rc ? rc : rc2;
+}
+
+/* phase B: the reference's whole combine tree for this rank's block */
+static int exec_phase_b(rank_exec_t *X, hipStream_t st)
+{
+    const mvx_plan *P = X->P;
+    const long E = P->esize;
+    const char *leafp[MVX_MAXP];
+    scratch_t S;
+    int s;
+    if (!P->has_combine || P->c_cnt == 0) return MPI_SUCCESS;
+    for (s = 0; s < P->p; s++)
+        leafp[s] = (s == P->rank) ? X->sendbuf + P->c_src_off * E : X->pool + X->slot[s];
+    S.base = X->pool + X->wide_off;
+    S.slot = X->wide_slot;
+    S.used = 0;
+    S.cap = X->wide_n;
+    return mvxi_combine(X->c, P, leafp, exec_out(X), &S, st);
+}
+
+/* phase C: combined blocks to the ranks that need them */
+static int exec_phase_c(rank_exec_t *X, mvx_xport *t, hipStream_t st)
+{
+    const mvx_plan *P = X->P;
+    const long E = P->esize;
+    int s, any = 0, rc = 0, rc2;
+    for (s = 0; s < P->p; s++) any |= (P->b_send[s].cnt || P->b_recv[s].cnt);
+    if (!any) return MPI_SUCCESS;
+    if ((rc = t->start(t))) return rc;
+    for (s = 0; s < P->p && !rc; s++) {
+        if (P->b_send[s].cnt)
+            rc = t->send(t, exec_out(X), (size_t)(P->b_send[s].cnt * E), s, st);
+        if (!rc && P->b_recv[s].cnt)
+            rc = t->recv(t, X->recvbuf + P->b_recv[s].off * E, (size_t)(P->b_recv[s].cnt * E), s, st);
+    }
+    rc2 = t->end(t);
+    return rc ? rc : rc2;
+}
+
+/* every local rank through phases A, B, C: one rank over RCCL, or all ranks
+ * of a virtual communicator over the loopback transport (whose transfers
+ * are paired once every rank has issued its phase) */
+int mvxi_exec_group(rank_exec_t *X, mvx_xport *t, int nr, hipStream_t st, mvx_comm_t *timed)
+{
+    int r, rc;
+    if (timed && (rc = mvxi_tev(timed, 0, st))) return rc;
+    for (r = 0; r < nr; r++)
+        if ((rc = exec_phase_a(&X[r], &t[r], st))) return rc;
+    if (t[0].lb && (rc = mvxi_lb_flush(t[0].lb, st))) return rc;
+    if (timed && (rc = mvxi_tev(timed, 1, st))) return rc;
+    for (r = 0; r < nr; r++)
+        if ((rc = exec_phase_b(&X[r], st))) return rc;
+    if (timed && (rc = mvxi_tev(timed, 2, st))) return rc;
+    for (r = 0; r < nr; r++)
+        if ((rc = exec_phase_c(&X[r], &t[r], st))) return rc;
+    if (t[0].lb && (rc = mvxi_lb_flush(t[0].lb, st))) return rc;
+    if (timed && (rc = mvxi_tev(timed, 3, st))) return rc;
+    if (timed && timed->timing) timed->tev_kind = TEV_PHASES;
+    return MPI_SUCCESS;
+}
+
+/* ---- slices ------------------------------------------------------------
+ * Slice i of a plan restricts every range to [i*cs, (i+1)*cs) relative to
+ * its own start.  Matched send / receive ranges have equal counts on both
+ * sides, so their slices stay matched; the combine range, its staging slots
+ * and the combined block slice together.  Block boundaries (the
+ * cnts[i] = n/pof2 of intra_fns_new.c:5645-5651) are untouched, so every
+ * element keeps its leaves, order and operand roles: slicing changes when a
+ * byte moves, never what is computed. */
+static void slice_range(mvx_range *r, long lo, long cs)
+{
+    long c = r->cnt - lo;
+    if (c > cs) c = cs;
+    if (c <= 0) { r->off = 0; r->cnt = 0; }
+    else r->off += lo;
+    if (c > 0) r->cnt = c;
+}
+
+void mvxi_plan_slice(const mvx_plan *P, long i, long cs, mvx_plan *Q)
+{
+    const long lo = i * cs;
+    long c = P->c_cnt - lo;
+    int s;
+    *Q = *P;
+    for (s = 0; s < P->p; s++) {
+        slice_range(&Q->a_send[s], lo, cs);
+        slice_range(&Q->a_recv[s], lo, cs);
+        slice_range(&Q->b_send[s], lo, cs);
+        slice_range(&Q->b_recv[s], lo, cs);
+    }
+    if (c > cs) c = cs;
+    if (c < 0) c = 0;
+    Q->c_cnt = c;
+    Q->c_src_off = P->c_src_off + lo;
+    Q->c_dst_off = P->c_dst_off + lo;
+}
+
+/* the longest range of a plan (slices needed = ceil(span / cs)) */
+long mvxi_plan_span(const mvx_plan *P)
+{
+    long m = P->has_combine ? P->c_cnt : 0;
+    int s;
+    for (s = 0; s < P->p; s++) {
+        if (P->a_send[s].cnt > m) m = P->a_send[s].cnt;
+        if (P->a_recv[s].cnt > m) m = P->a_recv[s].cnt;
+        if (P->b_send[s].cnt > m) m = P->b_send[s].cnt;
+        if (P->b_recv[s].cnt > m) m = P->b_recv[s].cnt;
+    }
+    return m;
+}
+
+/* ranges of sendbuf a plan reads and of recvbuf it writes, without repeats */
+static void add_range(mvx_range *v, int *n, long off, long cnt)
+{
+    int i;
+    if (cnt <= 0) return;
+    for (i = 0; i < *n; i++)
+        if (v[i].off == off && v[i].cnt == cnt) return;
+    v[*n].off = off;
+    v[*n].cnt = cnt;
+    (*n)++;
+}
+
+int mvxi_send_ranges(const mvx_plan *Q, mvx_range *v)
+{
+    int n = 0, s;
+    for (s = 0; s < Q->p; s++) add_range(v, &n, Q->a_send[s].off, Q->a_send[s].cnt);
+    if (Q->has_combine) add_range(v, &n, Q->c_src_off, Q->c_cnt);
+    return n;
+}
+
+int mvxi_recv_ranges(const mvx_plan *Q, mvx_range *v)
+{
+    int n = 0, s;
+    if (Q->has_combine && !Q->c_dst_tmp) add_range(v, &n, Q->c_dst_off, Q->c_cnt);
+    for (s = 0; s < Q->p; s++) add_range(v, &n, Q->b_recv[s].off, Q->b_recv[s].cnt);
+    return n;
+}
+
+
+/* the buffers' kinds, one pointer query each (pageable ranges may come back
+ * pinned from the registration cache); returns 1 if any is host memory */
+int mvxi_job_kinds(job_t *J)
+{
+    int r, host = 0;
+    if (!J->kinds) {
+        for (r = 0; r < J->nr; r++) {
+            const size_t E = (size_t)J->P[r].esize;
+            J->skind[r] = J->nsend[r] > 0 ? mvxi_buf_kind_range(J->send[r], (size_t)J->nsend[r] * E)
+                                          : MVX_BUF_DEVICE;
+            J->rkind[r] = J->nrecv[r] > 0 ? mvxi_buf_kind_range(J->recv[r], (size_t)J->nrecv[r] * E)
+                                          : MVX_BUF_DEVICE;
+        }
+        J->kinds = 1;
+    }
+    for (r = 0; r < J->nr; r++) host |= J->skind[r] != MVX_BUF_DEVICE || J->rkind[r] != MVX_BUF_DEVICE;
+    return host;
+}
+
+
+/* every local rank's staging region for plans Q: X[r].P / c set, per-rank
+ * offsets in off[], total bytes returned (pool not touched) */
+size_t mvxi_region_layout(mvx_comm_t *c, rank_exec_t *X, const job_t *J, const mvx_plan *Q, size_t *off)
+{
+    size_t need = 0;
+    int r;
+    for (r = 0; r < J->nr; r++) {
+        X[r].P = &Q[r];
+        X[r].c = c;
+        off[r] = (need + 255) & ~(size_t)255;
+        need = off[r] + exec_layout(&X[r]);
+    }
+    return (need + 255) & ~(size_t)255;
+}
+
+int mvxi_job_layout(mvx_comm_t *c, rank_exec_t *X, const job_t *J, const mvx_plan *Q)
+{
+    size_t off[MVX_MAXP];
+    const size_t need = mvxi_region_layout(c, X, J, Q, off);
+    int r, rc;
+    if ((rc = mvxi_grow(&c->pool, &c->pool_bytes, need))) return rc;
+    for (r = 0; r < J->nr; r++) X[r].pool = c->pool + off[r];
+    return MPI_SUCCESS;
+}
+
+/* ---- exchange variants (MVX_EXCH_*) -------------------------------------
+ * PIPE: the plan runs in slices; slice t's exchange and slice t-2's
+ * distribution go in one transfer group while slice t-1 is combined on a
+ * second stream, so xGMI and HBM work at once.  Slices keep every block
+ * boundary (plan_slice), so the bits are the unsliced plan's.  The slice
+ * plans and per-slice rank tables are the communicator's (mvx_work). */
+
+static int pipe_streams(mvx_comm_t *c)
+{
+    int i;
+    if (c->cstream) return MPI_SUCCESS;
+    if (hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking) != hipSuccess) return MPI_ERR_OTHER;
+    for (i = 0; i < 4; i++)
+        if (hipEventCreateWithFlags(&c->pev[i], hipEventDisableTiming) != hipSuccess) return MPI_ERR_OTHER;
+    return MPI_SUCCESS;
+}
+
+static int run_device_plain(mvx_comm_t *c, const job_t *J, hipStream_t st)
+{
+    rank_exec_t X[MVX_MAXP];
+    int r, rc;
+    for (r = 0; r < J->nr; r++) {
+        X[r].sendbuf = J->send[r];
+        X[r].recvbuf = J->recv[r];
+    }
+    if ((rc = mvxi_job_layout(c, X, J, J->P))) return rc;
+    return mvxi_exec_group(X, J->t, J->nr, st, c);
+}
+
+static int run_device_pipe(mvx_comm_t *c, const job_t *J, hipStream_t st)
+{
+    mvx_work *w = mvxi_work(c);
+    rank_exec_t *X0, (*X)[MVX_MAXP];
+    mvx_plan (*pl)[MVX_MAXP];
+    size_t off[MVX_MAXP], region;
+    long span = 0, cs, nsl, t;
+    int r, rc, q;
+    const int ns = c->exch_slices > 0 ? c->exch_slices : 4;
+    if (!w) return MPI_ERR_INTERN;
+    X0 = w->px0; X = w->px; pl = w->pipe;
+    for (r = 0; r < J->nr; r++)
+        if (mvxi_plan_span(&J->P[r]) > span) span = mvxi_plan_span(&J->P[r]);
+    cs = (span + ns - 1) / ns;
+    cs = (cs + 255) & ~255L;
+    nsl = (span + cs - 1) / cs;
+    if (nsl <= 1) return run_device_plain(c, J, st);
+    if ((rc = pipe_streams(c))) return rc;
+    c->ran_exch = MVX_EXCH_PIPE;
+    for (r = 0; r < J->nr; r++) {
+        mvxi_plan_slice(&J->P[r], 0, cs, &pl[0][r]);
+        X0[r].sendbuf = J->send[r];
+        X0[r].recvbuf = J->recv[r];
+    }
+    region = mvxi_region_layout(c, X0, J, pl[0], off);   /* slice 0 is the largest */
+    if ((rc = mvxi_grow(&c->pool, &c->pool_bytes, 2 * region))) return rc;
+    if ((rc = mvxi_tev(c, 0, st))) return rc;
+    for (t = 0; t < nsl + 2; t++) {
+        const int a = t < nsl, dist = t >= 2;
+        const int cur = (int)(t % 3), old = (int)((t + 1) % 3);   /* old = (t - 2) % 3 */
+        if (a)
+            for (r = 0; r < J->nr; r++) {
+                X[cur][r] = X0[r];
+                mvxi_plan_slice(&J->P[r], t, cs, &pl[cur][r]);
+                X[cur][r].P = &pl[cur][r];
+                X[cur][r].pool = c->pool + (t & 1) * region + off[r];
+            }
+        /* slice t-2's combine is done before its blocks leave and before
+         * slice t reuses its staging region */
+        if (dist && hipStreamWaitEvent(st, c->pev[2 + (int)(t & 1)], 0) != hipSuccess) return MPI_ERR_OTHER;
+        for (r = 0; r < J->nr; r++) {
+            mvx_xport *x = &J->t[r];
+            if ((rc = x->start(x))) return rc;
+            if (a && (rc = exec_phase_a(&X[cur][r], x, st))) return rc;
+            if (dist && (rc = exec_phase_c(&X[old][r], x, st))) return rc;
+            if ((rc = x->end(x))) return rc;
+        }
+        if (J->t[0].lb && (rc = mvxi_lb_flush(J->t[0].lb, st))) return rc;
+        if (!a) continue;
+        if (hipEventRecord(c->pev[t & 1], st) != hipSuccess ||
+            hipStreamWaitEvent(c->cstream, c->pev[t & 1], 0) != hipSuccess)
+            return MPI_ERR_OTHER;
+        for (q = 0; q < J->nr; q++)
+            if ((rc = exec_phase_b(&X[cur][q], c->cstream))) return rc;
+        if (hipEventRecord(c->pev[2 + (int)(t & 1)], c->cstream) != hipSuccess) return MPI_ERR_OTHER;
+    }
+    if ((rc = mvxi_tev(c, 3, st))) return rc;
+    if (c->timing) c->tev_kind = TEV_TOTAL;
+    return MPI_SUCCESS;
+}
+
+/* COLL: a regular plan -- every rank holds p equal blocks in rank order and
+ * combines block `rank` -- exchanges with ncclAllToAll and (Allreduce)
+ * distributes with an in-place ncclAllGather instead of grouped send /
+ * receive.  Every rank sees the same count and size, so all ranks choose
+ * the same variant. */
+static int coll_regular(const mvx_plan *P, long *blk)
+{
+    const long b = P->c_cnt;
+    int s;
+    if (P->p < 2 || !P->has_combine || b <= 0 || P->c_dst_tmp) return 0;
+    if (P->coll != MVX_COLL_ALLREDUCE && P->coll != MVX_COLL_REDUCE_SCATTER) return 0;
+    if (P->count != b * P->p || P->c_src_off != b * P->rank) return 0;
+    if (P->c_dst_off != (P->coll == MVX_COLL_ALLREDUCE ? b * P->rank : 0)) return 0;
+    for (s = 0; s < P->p; s++) {
+        if (s == P->rank) continue;
+        if (P->a_send[s].off != b * s || P->a_send[s].cnt != b) return 0;
+        if (P->a_recv[s].off != b * P->rank || P->a_recv[s].cnt != b) return 0;
+        if (P->coll == MVX_COLL_ALLREDUCE) {
+            if (P->b_send[s].off != b * P->rank || P->b_send[s].cnt != b) return 0;
+            if (P->b_recv[s].off != b * s || P->b_recv[s].cnt != b) return 0;
+        } else if (P->b_send[s].cnt || P->b_recv[s].cnt) {
+            return 0;
+        }
+    }
+    *blk = b;
+    return 1;
+}
+
+static int run_device_coll(mvx_comm_t *c, const job_t *J, long b, hipStream_t st)
+{
+    const mvx_plan *P = &J->P[0];
+    mvx_xport *t = &J->t[0];
+    const size_t bb = (size_t)(b * P->esize);
+    const char *leafp[MVX_MAXP];
+    rank_exec_t X;
+    scratch_t S;
+    size_t stage;
+    int s, rc;
+    X.P = P; X.c = c; X.sendbuf = J->send[0]; X.recvbuf = J->recv[0];
+    stage = al256(bb * (size_t)P->p);
+    X.wide_n = mvxi_wide_temps(P);
+    X.wide_slot = al256(bb + SLOT_STAGGER);
+    if ((rc = mvxi_grow(&c->pool, &c->pool_bytes, stage + X.wide_slot * (size_t)X.wide_n))) return rc;
+    c->ran_exch = MVX_EXCH_COLL;
+    if ((rc = mvxi_tev(c, 0, st))) return rc;
+    if ((rc = t->alltoall(t, J->send[0], c->pool, bb, st))) return rc;
+    if ((rc = mvxi_tev(c, 1, st))) return rc;
+    for (s = 0; s < P->p; s++)
+        leafp[s] = s == P->rank ? J->send[0] + (size_t)P->rank * bb : c->pool + (size_t)s * bb;
+    S.base = c->pool + stage; S.slot = X.wide_slot; S.used = 0; S.cap = X.wide_n;
+    if ((rc = mvxi_combine(c, P, leafp, J->recv[0] + P->c_dst_off * P->esize, &S, st))) return rc;
+    if ((rc = mvxi_tev(c, 2, st))) return rc;
+    if (P->coll == MVX_COLL_ALLREDUCE && (rc = t->allgather(t, J->recv[0], bb, st))) return rc;
+    if ((rc = mvxi_tev(c, 3, st))) return rc;
+    if (c->timing) c->tev_kind = TEV_PHASES;
+    return MPI_SUCCESS;
+}
+
+/* all buffers in HBM */
+int mvxi_run_device(mvx_comm_t *c, const job_t *J, hipStream_t st)
+{
+    long blk;
+    c->ran_exch = MVX_EXCH_P2P;   /* unless a variant below takes the call */
+    if (c->exch == MVX_EXCH_PIPE) return run_device_pipe(c, J, st);
+    if (c->exch == MVX_EXCH_COLL && J->nr == 1 && J->t[0].alltoall && J->t[0].allgather &&
+        J->P[0].opkind == MVX_OPKIND_PREDEFINED && coll_regular(&J->P[0], &blk))
+        return run_device_coll(c, J, blk, st);
+    return run_device_plain(c, J, st);
+}

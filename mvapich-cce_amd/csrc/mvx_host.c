@@ -11,12 +11,19 @@
  *                        bounce slots by host cores while the DMA engines
  *                        move the previous / next slice over PCIe.
  *
- * Why bounce buffers and not a registration cache: a cached hipHostRegister
- * of a user buffer goes stale when the user frees the buffer and malloc
- * hands the same range out again (MVAPICH's dreg needs malloc hooks for
- * that); registering per call costs about as much as the copy itself
- * (tools/h2d_probe.c: 4.6 ms per 256 MiB).  Callers that keep a buffer for
- * long can pin it themselves and get the zero-copy DMA path.
+ * Registration cache (opt-in: MVX_HOST_REGISTER=1, or
+ * mvx_host_register_enable).  MVAPICH pins a user buffer once and reuses
+ * the registration (mpid/ch_gen2/dreg.c:774-832, dreg_register / dreg_find);
+ * here a pageable range a call uses is hipHostRegister'ed on first use and
+ * kept, so later calls on it DMA directly instead of copying through the
+ * bounce slots.  Entries are page-aligned [base, end) ranges, evicted least
+ * recently used past MVX_HOST_REGISTER_MAX_MIB (default 16384); ranges under
+ * MVX_HOST_REGISTER_MIN_KIB (default 1024) are never registered.  The
+ * reference learns of freed memory through malloc hooks (mem_hooks.c); here
+ * the contract is mvx_host_unregister(addr) before the memory is freed.
+ * (What the driver does when a registered range is unmapped and mapped
+ * again without the call is measured, not assumed: DESIGN.md section 5a,
+ * tests/test_gpu_host_register.py.)
  */
 #include <pthread.h>
 #include <stdint.h>
@@ -163,4 +170,137 @@ int mvx_copy_threads(void)
     n = g_pc.nworkers + 1;
     pthread_mutex_unlock(&g_pc.mu);
     return n;
+}
+
+/* ---- the registration cache ------------------------------------------------ */
+
+#define REG_MAX 64
+#define PAGE 4096UL
+typedef struct { uintptr_t base, end; unsigned long stamp; } reg_t;
+static struct {
+    pthread_mutex_t mu;
+    int init, on;
+    size_t min_bytes, max_bytes, total;
+    unsigned long clock, hits, misses, evictions, failures;
+    int n;
+    reg_t e[REG_MAX];
+} g_reg = { PTHREAD_MUTEX_INITIALIZER, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, {{0, 0, 0}} };
+
+static void reg_env(void)
+{
+    const char *v;
+    if (g_reg.init) return;
+    g_reg.init = 1;
+    v = getenv("MVX_HOST_REGISTER");
+    g_reg.on = v && atoi(v) == 1;
+    v = getenv("MVX_HOST_REGISTER_MIN_KIB");
+    g_reg.min_bytes = (size_t)(v ? atol(v) : 1024) << 10;
+    v = getenv("MVX_HOST_REGISTER_MAX_MIB");
+    g_reg.max_bytes = (size_t)(v ? atol(v) : 16384) << 20;
+}
+
+static void reg_drop(int i)
+{
+    (void)hipHostUnregister((void *)g_reg.e[i].base);
+    (void)hipGetLastError();
+    g_reg.total -= g_reg.e[i].end - g_reg.e[i].base;
+    g_reg.e[i] = g_reg.e[--g_reg.n];
+}
+
+static void reg_drop_all(void)
+{
+    while (g_reg.n) reg_drop(g_reg.n - 1);
+}
+
+int mvx_host_register_enable(int on, size_t max_bytes)
+{
+    pthread_mutex_lock(&g_reg.mu);
+    reg_env();
+    g_reg.on = on ? 1 : 0;
+    if (max_bytes) g_reg.max_bytes = max_bytes;
+    if (!g_reg.on) reg_drop_all();
+    pthread_mutex_unlock(&g_reg.mu);
+    return 0;
+}
+
+int mvx_host_unregister(const void *addr)
+{
+    const uintptr_t a = (uintptr_t)addr;
+    int i, found = 0;
+    pthread_mutex_lock(&g_reg.mu);
+    for (i = g_reg.n - 1; i >= 0; i--)
+        if (g_reg.e[i].base <= a && a < g_reg.e[i].end) { reg_drop(i); found = 1; }
+    pthread_mutex_unlock(&g_reg.mu);
+    return found ? 0 : MPI_ERR_ARG;
+}
+
+int mvx_host_register_stats(long *entries, size_t *bytes, long *hits, long *misses)
+{
+    pthread_mutex_lock(&g_reg.mu);
+    if (entries) *entries = g_reg.n;
+    if (bytes) *bytes = g_reg.total;
+    if (hits) *hits = (long)g_reg.hits;
+    if (misses) *misses = (long)g_reg.misses;
+    pthread_mutex_unlock(&g_reg.mu);
+    return 0;
+}
+
+int mvxi_buf_kind_range(const void *p, size_t bytes)
+{
+    const int k = mvx_buf_kind(p);
+    uintptr_t base, end;
+    int i, cover = -1, overlap = 0;
+    if (k == MVX_BUF_DEVICE || !p || !bytes) return k;
+    pthread_mutex_lock(&g_reg.mu);
+    reg_env();
+    if (!g_reg.on && !g_reg.n) { pthread_mutex_unlock(&g_reg.mu); return k; }
+    base = (uintptr_t)p & ~(PAGE - 1);
+    end = ((uintptr_t)p + bytes + PAGE - 1) & ~(PAGE - 1);
+    for (i = 0; i < g_reg.n; i++) {
+        if (g_reg.e[i].base <= base && end <= g_reg.e[i].end) cover = i;
+        else if (g_reg.e[i].base < end && base < g_reg.e[i].end) overlap = 1;
+    }
+    if (cover >= 0) {                                   /* dreg_find */
+        g_reg.e[cover].stamp = ++g_reg.clock;
+        g_reg.hits++;
+        pthread_mutex_unlock(&g_reg.mu);
+        return MVX_BUF_PINNED;
+    }
+    if (k == MVX_BUF_PINNED && !overlap) {              /* the caller's own page-locked memory */
+        pthread_mutex_unlock(&g_reg.mu);
+        return k;
+    }
+    /* a range that runs past a registration of ours: the union replaces it
+     * (a DMA must never read past the pinned pages) */
+    for (i = g_reg.n - 1; i >= 0; i--)
+        if (g_reg.e[i].base < end && base < g_reg.e[i].end) {
+            if (g_reg.e[i].base < base) base = g_reg.e[i].base;
+            if (g_reg.e[i].end > end) end = g_reg.e[i].end;
+            reg_drop(i);
+        }
+    if (!g_reg.on || end - base < g_reg.min_bytes || end - base > g_reg.max_bytes) {
+        pthread_mutex_unlock(&g_reg.mu);
+        return mvx_buf_kind(p);
+    }
+    while (g_reg.n && (g_reg.n == REG_MAX || g_reg.total + (end - base) > g_reg.max_bytes)) {
+        int lru = 0;                                    /* evict the least recently used */
+        for (i = 1; i < g_reg.n; i++)
+            if (g_reg.e[i].stamp < g_reg.e[lru].stamp) lru = i;
+        reg_drop(lru);
+        g_reg.evictions++;
+    }
+    g_reg.misses++;
+    if (hipHostRegister((void *)base, end - base, hipHostRegisterDefault) != hipSuccess) {   /* dreg_register */
+        (void)hipGetLastError();
+        g_reg.failures++;
+        pthread_mutex_unlock(&g_reg.mu);
+        return mvx_buf_kind(p);
+    }
+    g_reg.e[g_reg.n].base = base;
+    g_reg.e[g_reg.n].end = end;
+    g_reg.e[g_reg.n].stamp = ++g_reg.clock;
+    g_reg.n++;
+    g_reg.total += end - base;
+    pthread_mutex_unlock(&g_reg.mu);
+    return MVX_BUF_PINNED;
 }
