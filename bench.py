@@ -43,7 +43,18 @@ CONFIGS = {
     "c4": ("reduce_scatter", MPI_LONG, MPI_BAND, 8, 1024, "MPI_Reduce_scatter MPI_BAND MPI_LONG"),
     "c5": ("allreduce", MPI_FLOAT_INT, MPI_MAXLOC, 8, 512, "MPI_Allreduce MPI_MAXLOC MPI_FLOAT_INT"),
 }
-EXCH = {"p2p": (0, 0), "pipe": (1, 4), "pipe2": (1, 2), "pipe8": (1, 8), "coll": (2, 0)}
+# exchange variants: (mvx_comm_set_exchange mode, slices, mvx_comm_set_graphs).
+# The "+g" ones capture each call into a HIP graph once and replay it (one
+# hipGraphLaunch per step in place of the host issue of every RCCL group and
+# kernel); tried last, after every eager variant has had its turn.
+EXCH = {"p2p": (0, 0, 0), "pipe": (1, 4, 0), "pipe2": (1, 2, 0), "pipe8": (1, 8, 0), "coll": (2, 0, 0),
+        "p2p+g": (0, 0, 1), "pipe+g": (1, 4, 1), "pipe2+g": (1, 2, 1), "pipe8+g": (1, 8, 1), "coll+g": (2, 0, 1)}
+
+
+def apply_variant(comm, name):
+    """set the communicator's exchange variant and graph mode: 0 or an MPI code"""
+    mode, slices, graphs = EXCH[name]
+    return comm.set_exchange(mode, slices) or comm.set_graphs(graphs)
 
 
 def parse(argv=None):
@@ -72,7 +83,9 @@ def parse(argv=None):
     ap.add_argument("--sets", type=int, default=4,
                     help="input sets used round-robin (4 x 512 MiB keeps every step out of the 256 MiB "
                          "Infinity Cache: the number is HBM-bound, not cache-bound)")
-    ap.add_argument("--exchange", default="auto", choices=["auto", "p2p", "pipe", "pipe2", "pipe8", "coll"])
+    ap.add_argument("--exchange", default="auto",
+                    help="auto: every variant (EXCH), the fastest clean one makes the line; or a comma list "
+                         "of them")
     ap.add_argument("--tune-steps", type=int, default=5)
     ap.add_argument("--extra-configs", default="auto",
                     help="N > 1: more BASELINE configs measured after the line, on the same communicator "
@@ -91,7 +104,12 @@ def parse(argv=None):
                          "share a GPU, bytes move through RCCL's own socket transport (each rank "
                          "names itself a separate host).  Both test the multi-GPU leg on a 1-GPU "
                          "box; neither is a performance configuration")
-    return ap.parse_args(argv)
+    args = ap.parse_args(argv)
+    if args.exchange != "auto":
+        bad = [x for x in args.exchange.split(",") if x not in EXCH]
+        if bad:
+            ap.error("--exchange: unknown variant(s) %s (known: %s)" % (",".join(bad), ",".join(EXCH)))
+    return args
 
 
 # ------------------------------------------------------------ wall clock --
@@ -706,6 +724,7 @@ def _wait_stream(stream, seconds, spin=False):
 
 
 EXCH_NAMES = {-1: "none", 0: "p2p", 1: "pipe", 2: "coll"}
+GRAPH_STATES = {0: "eager", 1: "replayed", 2: "captured"}
 
 
 def choose_variant(names, tried):
@@ -762,8 +781,7 @@ def run_extra(args, mvx, dev, world, rank, comm, exch_name, cfg, agree, stream):
     recvbuf = torch.empty(nrecv * E, dtype=torch.uint8, device=dev)
     cnts = [n // world] * world
     comm.reserve(2 * nbytes)
-    mode, slices = EXCH[exch_name]
-    comm.set_exchange(mode, slices)
+    apply_variant(comm, exch_name)
     out = {"config": cfg, "workload": "%s %d MiB per rank" % (desc, nbytes // MIB),
            "vector_bytes_per_rank": nbytes, "exchange": exch_name}
 
@@ -991,10 +1009,14 @@ def run_multi(args, mvx, dev, world, rank, local, clock):
         failure in the untimed phase steps is recorded in the line's phases
         and returned as its status."""
         cur["name"] = name
-        cur["comm"].set_exchange(*EXCH[name])
+        apply_variant(cur["comm"], name)
         limit = step_limit(args, est_s)
         times = timed(args, step, stream, world, agree, limit)
         ran = EXCH_NAMES.get(cur["comm"].last_exchange(), "?")
+        graph = GRAPH_STATES.get(cur["comm"].last_graph()[0]) if EXCH[name][2] else None
+        # set 0's result as the timed steps left it (graph replays included)
+        # against the reference again
+        post = parity_check()
         pb = plan_bytes(mvx, coll, world, rank, n, cnts, dtype, op)
         status = 0
         try:
@@ -1019,11 +1041,14 @@ def run_multi(args, mvx, dev, world, rank, local, clock):
                      {"workload": "%s: %s %d MiB per rank, RCCL xGMI exchange + reference-order combine"
                                   % (cfg, desc, nbytes // MIB),
                       "vector_bytes_per_rank": nbytes, "parallelism": "dp%d (blocks sharded over ranks)" % p,
-                      "exchange": name, "exchange_ran": ran, "exchange_tuning": None,
+                      "exchange": name, "exchange_ran": ran, "graph": graph, "exchange_tuning": None,
                       "transport": args.transport}, roof)
         parity = tried[name]["parity"]
+        if post is False:
+            parity = False
         out["parity"] = (("bit-exact vs the reference schedule, all %d ranks" % p) if parity
                          else ("MISMATCH" if parity is False else None))
+        out["parity_after_timed"] = post
         out["cpu_baseline"] = cpu
         return out, status
 
@@ -1037,13 +1062,13 @@ def run_multi(args, mvx, dev, world, rank, local, clock):
     # measured again only if its tuning steps ran faster -- so a line exists
     # before any riskier variant runs, and a variant that wedges the GPU for
     # good ends the run with the line already measured rather than with none.
-    names = list(EXCH) if args.exchange == "auto" else [args.exchange]
+    names = list(EXCH) if args.exchange == "auto" else args.exchange.split(",")
     tried = {}
 
     for name in names:
-        mode, slices = EXCH[name]
+        mode = EXCH[name][0]
         cur["name"] = name
-        status = 1 if cur["comm"].set_exchange(mode, slices) else 0
+        status = 1 if apply_variant(cur["comm"], name) else 0
         est = 0.0
         if agree(status) == 0:
             it[0] = 0
@@ -1065,10 +1090,18 @@ def run_multi(args, mvx, dev, world, rank, local, clock):
             clock.mark("variant %s" % name)
             continue
         t = torch.zeros(1, dtype=torch.float64)
+        terr = 0
+        if EXCH[name][2]:
+            # graphs: each input set's first call ran eagerly, its second is
+            # captured -- untimed here, so the tuning steps are replays
+            try:
+                for _ in range(2 * sets):
+                    step()
+            except RuntimeError:
+                terr = 1
         torch.cuda.synchronize()
         dist.barrier()
         t0 = time.perf_counter()
-        terr = 0
         issue = []
         for _ in range(args.tune_steps):      # every rank issues every step
             t1 = time.perf_counter()
@@ -1098,6 +1131,11 @@ def run_multi(args, mvx, dev, world, rank, local, clock):
         torch.cuda.synchronize()
         entry.update(ms_per_step=round(float(t.item()) * 1e3 / args.tune_steps, 4), parity=ok,
                      host_issue_us=round(float(hi.item()) * 1e6, 1))
+        if EXCH[name][2]:
+            # what the last tuning step was: a replayed graph (1), a capture (2)
+            # or an eager call (0: graphs off on this communicator, see error)
+            gs, ge = cur["comm"].last_graph()
+            entry["graph"] = {"state": GRAPH_STATES.get(gs, gs), "capture_error": ge}
         # measure for the line: the first clean variant, then any that tuned
         # faster than the one measured (every rank decides alike: the tuning
         # time is the MAX over ranks and parity is compared on every rank)
@@ -1113,7 +1151,9 @@ def run_multi(args, mvx, dev, world, rank, local, clock):
                 recover(e.worst, entry)
                 clock.mark("variant %s" % name)
                 continue
-            if best is None or cand["ms_per_step"] < best["ms_per_step"]:
+            if cand.get("parity_after_timed") is False:
+                entry.update(parity=False, error="MISMATCH in the result the timed steps left")
+            elif best is None or cand["ms_per_step"] < best["ms_per_step"]:
                 cur["best"] = cand
             if pstat:
                 entry["error"] = cand["roofline"]["phases"]["error"]

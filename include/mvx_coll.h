@@ -107,6 +107,19 @@ int mvx_comm_get_exchange(MPI_Comm comm, int *mode, int *slices);
  * host buffers or a transport without collectives; PIPE on a plan too small
  * to slice); -1 when the call moved nothing between ranks. */
 int mvx_comm_last_exchange(MPI_Comm comm, int *mode);
+/* Device calls as HIP graphs (default off; env at creation MVX_GRAPH=1).
+ * On an RCCL communicator, a device-buffer call with a predefined op whose
+ * job (plan, buffers, stream, variant) was seen before is captured into a
+ * graph once and replayed after: one hipGraphLaunch in place of the host
+ * issue of every transfer group and kernel (the PIPE variant's slices
+ * especially).  The first call of a job runs eagerly, the second captures
+ * and launches, later ones replay.  Same bits as the eager calls.  A failed
+ * capture turns graphs off on the communicator (mvx_comm_last_graph reports
+ * the error); mvx_comm_set_graphs(comm, 0) drops every graph. */
+int mvx_comm_set_graphs(MPI_Comm comm, int on);
+/* The last call: *state 0 eager, 1 replayed, 2 captured and launched;
+ * *error the failed capture's code that turned graphs off (0: none). */
+int mvx_comm_last_graph(MPI_Comm comm, int *state, int *error);
 /* Tear down a communicator without waiting for its outstanding transfers
  * (ncclCommAbort): the way out of a transfer that never completes.  The
  * handle is freed as by mvx_comm_free; the staging memory is not (work

@@ -135,6 +135,8 @@ def _load():
     c.mvx_comm_init_transport.argtypes = [pi, i, i, i, vp]
     c.mvx_comm_init_transport_ex.argtypes = [pi, i, i, i, vp, sz]
     c.mvx_comm_set_host_pipeline.argtypes = [i, i]
+    c.mvx_comm_set_graphs.argtypes = [i, i]
+    c.mvx_comm_last_graph.argtypes = [i, pi, pi]
     c.mvx_comm_reap.argtypes = []
     c.mvx_host_register_enable.argtypes = [i, sz]
     c.mvx_host_unregister.argtypes = [vp]

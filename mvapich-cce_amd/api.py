@@ -170,6 +170,20 @@ class Comm:
         then pass host buffers) instead of HBM mirrors (mvx_comm_set_host_pipeline)."""
         return coll().mvx_comm_set_host_pipeline(self.handle, 1 if on else 0)
 
+    def set_graphs(self, on=True):
+        """Capture device calls into HIP graphs and replay them (mvx_comm_set_graphs)."""
+        return coll().mvx_comm_set_graphs(self.handle, 1 if on else 0)
+
+    def last_graph(self):
+        """(state, error) of the last call (mvx_comm_last_graph): state 0
+        eager, 1 replayed, 2 captured and launched; error the failed
+        capture's code that turned graphs off (0: none)."""
+        st, err = ctypes.c_int(), ctypes.c_int()
+        rc = coll().mvx_comm_last_graph(self.handle, ctypes.byref(st), ctypes.byref(err))
+        if rc:
+            raise RuntimeError("mvx_comm_last_graph rc=%d" % rc)
+        return st.value, err.value
+
     def set_stream(self, stream=None):
         return coll().mvx_comm_set_stream(self.handle, stream_handle(stream))
 

@@ -135,7 +135,8 @@ static int claim_shmem_block(void)
 }
 
 /* MVX_EXCHANGE = p2p | pipe[:slices] | coll (default p2p);
- * MVX_HOST_PIPELINE = 1: host buffers at p > 1 take the sliced pipeline */
+ * MVX_HOST_PIPELINE = 1: host buffers at p > 1 take the sliced pipeline;
+ * MVX_GRAPH = 1: device calls are captured and replayed as HIP graphs */
 static void exchange_from_env(mvx_comm_t *c)
 {
     const char *e = getenv("MVX_EXCHANGE");
@@ -143,6 +144,7 @@ static void exchange_from_env(mvx_comm_t *c)
     c->exch = MVX_EXCH_P2P;
     c->exch_slices = 4;
     c->host_sliced = env_int("MVX_HOST_PIPELINE", &v) && v == 1;
+    c->graphs = env_int("MVX_GRAPH", &v) && v == 1;
     if (!e) return;
     if (!strncmp(e, "pipe", 4)) {
         c->exch = MVX_EXCH_PIPE;
@@ -379,6 +381,14 @@ static int comm_release(MPI_Comm *comm, int abort)
         if (c->xpool) hipFree(c->xpool);
         if (c->w) mvxi_stage_release(&c->w->stage);
     }
+    /* an aborted communicator's graphs may still be running: left to the
+     * process, like any work queued behind its transfers */
+    if (!abort) mvxi_graphs_clear(c);
+    if (c->gstream) {
+        hipStreamDestroy(c->gstream);
+        hipEventDestroy(c->gev[0]);
+        hipEventDestroy(c->gev[1]);
+    }
     if (c->cstream) hipStreamDestroy(c->cstream);
     if (c->pev[0])
         for (i = 0; i < 4; i++) hipEventDestroy(c->pev[i]);
@@ -458,6 +468,25 @@ int mvx_comm_set_host_pipeline(MPI_Comm comm, int on)
     mvx_comm_t *c = mvxi_get_comm(comm);
     if (!c) return ERR_COMM_NULL_CODE;
     c->host_sliced = on ? 1 : 0;
+    return MPI_SUCCESS;
+}
+
+int mvx_comm_set_graphs(MPI_Comm comm, int on)
+{
+    mvx_comm_t *c = mvxi_get_comm(comm);
+    if (!c) return ERR_COMM_NULL_CODE;
+    if (!on) mvxi_graphs_clear(c);
+    c->graphs = on ? 1 : 0;
+    c->graph_error = 0;
+    return MPI_SUCCESS;
+}
+
+int mvx_comm_last_graph(MPI_Comm comm, int *state, int *error)
+{
+    mvx_comm_t *c = mvxi_get_comm(comm);
+    if (!c) return ERR_COMM_NULL_CODE;
+    if (state) *state = c->last_graph;
+    if (error) *error = c->graph_error;
     return MPI_SUCCESS;
 }
 
@@ -564,9 +593,12 @@ int mvx_comm_set_stream(MPI_Comm comm, void *stream)
 
 /* ---- staging pools --------------------------------------------------------- */
 
+__thread int mvxi_capturing;
+
 int mvxi_grow(char **buf, size_t *have, size_t need)
 {
     if (need <= *have) return MPI_SUCCESS;
+    if (mvxi_capturing) return MPI_ERR_OTHER;   /* no reallocation inside a graph capture */
     if (*buf) { hipDeviceSynchronize(); hipFree(*buf); *buf = NULL; *have = 0; }
     need = (need + (1 << 20) - 1) & ~(size_t)((1 << 20) - 1);
     if (hipMalloc((void **)buf, need) != hipSuccess) { *buf = NULL; return MPI_ERR_OTHER; }
@@ -577,6 +609,7 @@ int mvxi_grow(char **buf, size_t *have, size_t need)
 int mvxi_grow_host(char **buf, size_t *have, size_t need)
 {
     if (need <= *have) return MPI_SUCCESS;
+    if (mvxi_capturing) return MPI_ERR_OTHER;
     if (*buf) { hipHostFree(*buf); *buf = NULL; *have = 0; }
     need = (need + (1 << 20) - 1) & ~(size_t)((1 << 20) - 1);
     if (hipHostMalloc((void **)buf, need, hipHostMallocDefault) != hipSuccess) { *buf = NULL; return MPI_ERR_OTHER; }

@@ -399,7 +399,7 @@ static int run_device_coll(mvx_comm_t *c, const job_t *J, long b, hipStream_t st
 }
 
 /* all buffers in HBM */
-int mvxi_run_device(mvx_comm_t *c, const job_t *J, hipStream_t st)
+static int run_device_eager(mvx_comm_t *c, const job_t *J, hipStream_t st)
 {
     long blk;
     c->ran_exch = MVX_EXCH_P2P;   /* unless a variant below takes the call */
@@ -408,4 +408,157 @@ int mvxi_run_device(mvx_comm_t *c, const job_t *J, hipStream_t st)
         J->P[0].opkind == MVX_OPKIND_PREDEFINED && coll_regular(&J->P[0], &blk))
         return run_device_coll(c, J, blk, st);
     return run_device_plain(c, J, st);
+}
+
+/* ---- graphs (mvx_comm_set_graphs) ---------------------------------------
+ * The first call of a job runs eagerly (it also sizes the staging pool and
+ * opens RCCL's connections); the second is captured into a HIP graph on the
+ * call's stream -- RCCL's groups record their kernels, PIPE's combine stream
+ * joins through its events -- and launched; later ones replay it.  A
+ * capture that fails turns graphs off on the communicator (graph_error) and
+ * the call runs eagerly.  Null-stream calls capture and replay on the
+ * communicator's own stream, forked from and joined back to the null
+ * stream with events. */
+static unsigned long long graph_hash(const mvx_comm_t *c, const job_t *J, hipStream_t st)
+{
+    const unsigned char *b = (const unsigned char *)&J->P[0];
+    unsigned long long h = 1469598103934665603ull;
+    const uintptr_t v[6] = {(uintptr_t)J->send[0], (uintptr_t)J->recv[0], (uintptr_t)st, (uintptr_t)c->pool,
+                            (uintptr_t)(c->exch * 4096 + c->exch_slices), (uintptr_t)c->keep};
+    size_t i;
+    for (i = 0; i < sizeof(mvx_plan); i++) h = (h ^ b[i]) * 1099511628211ull;
+    for (i = 0; i < 6; i++) h = (h ^ v[i]) * 1099511628211ull;
+    return h;
+}
+
+static int graph_match(const graph_ent_t *g, const mvx_comm_t *c, const job_t *J, hipStream_t st,
+                       unsigned long long h)
+{
+    return g->state && g->hash == h && g->send == J->send[0] && g->recv == J->recv[0] && g->st == st &&
+           g->pool == c->pool && g->exch == c->exch && g->slices == c->exch_slices && g->keep == c->keep &&
+           !memcmp(&g->plan, &J->P[0], sizeof(mvx_plan));
+}
+
+static void graph_drop(graph_ent_t *g)
+{
+    if (g->state == 2 && g->exec) hipGraphExecDestroy(g->exec);
+    memset(g, 0, sizeof *g);
+}
+
+void mvxi_graphs_clear(mvx_comm_t *c)
+{
+    int i;
+    if (!c->w) return;
+    for (i = 0; i < GRAPH_CACHE; i++) graph_drop(&c->w->graphs[i]);
+}
+
+static int graph_eligible(const mvx_comm_t *c, const job_t *J)
+{
+    return c->graphs && !c->graph_error && J->nr == 1 && !c->local && !c->has_ops && c->nccl && !c->timing &&
+           J->P[0].opkind == MVX_OPKIND_PREDEFINED && !J->P[0].packed;
+}
+
+static int graph_streams(mvx_comm_t *c)
+{
+    if (c->gstream) return MPI_SUCCESS;
+    if (hipStreamCreateWithFlags(&c->gstream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&c->gev[0], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->gev[1], hipEventDisableTiming) != hipSuccess)
+        return MPI_ERR_OTHER;
+    return MPI_SUCCESS;
+}
+
+static int graph_launch(mvx_comm_t *c, hipGraphExec_t x, hipStream_t st)
+{
+    if (st) return hipGraphLaunch(x, st) == hipSuccess ? MPI_SUCCESS : MPI_ERR_OTHER;
+    if (hipEventRecord(c->gev[0], st) != hipSuccess || hipStreamWaitEvent(c->gstream, c->gev[0], 0) != hipSuccess ||
+        hipGraphLaunch(x, c->gstream) != hipSuccess || hipEventRecord(c->gev[1], c->gstream) != hipSuccess ||
+        hipStreamWaitEvent(st, c->gev[1], 0) != hipSuccess)
+        return MPI_ERR_OTHER;
+    return MPI_SUCCESS;
+}
+
+/* capture the job on `cs` into an executable graph (nothing runs) */
+static int graph_capture(mvx_comm_t *c, const job_t *J, hipStream_t cs, hipGraphExec_t *out)
+{
+    hipGraph_t g = NULL;
+    hipError_t e;
+    int rc;
+    *out = NULL;
+    if (hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal) != hipSuccess) {
+        (void)hipGetLastError();
+        return MPI_ERR_OTHER;
+    }
+    mvxi_capturing = 1;
+    rc = run_device_eager(c, J, cs);
+    mvxi_capturing = 0;
+    e = hipStreamEndCapture(cs, &g);
+    if (rc || e != hipSuccess || !g) {
+        if (g) hipGraphDestroy(g);
+        (void)hipGetLastError();
+        return rc ? rc : MPI_ERR_OTHER;
+    }
+    e = hipGraphInstantiate(out, g, NULL, NULL, 0);
+    hipGraphDestroy(g);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        *out = NULL;
+        return MPI_ERR_OTHER;
+    }
+    return MPI_SUCCESS;
+}
+
+static int run_device_graph(mvx_comm_t *c, const job_t *J, hipStream_t st)
+{
+    mvx_work *w = mvxi_work(c);
+    const unsigned long long h = graph_hash(c, J, st);
+    graph_ent_t *g = NULL, *lru = NULL;
+    hipGraphExec_t x;
+    int i, rc;
+    if (!w || (!st && graph_streams(c))) return run_device_eager(c, J, st);
+    for (i = 0; i < GRAPH_CACHE; i++) {
+        graph_ent_t *e = &w->graphs[i];
+        if (graph_match(e, c, J, st, h)) { g = e; break; }
+        if (e->state && e->pool != c->pool) graph_drop(e);     /* captured on a pool since reallocated */
+        if (!lru || !e->state || (lru->state && e->stamp < lru->stamp)) lru = e;
+    }
+    if (g && g->state == 2) {                                  /* replay */
+        g->stamp = ++w->graph_clock;
+        c->ran_exch = g->ran_exch;
+        c->last_graph = 1;
+        return graph_launch(c, g->exec, st);
+    }
+    if (!g) {                                                  /* first sighting: eager */
+        c->last_graph = 0;
+        rc = run_device_eager(c, J, st);
+        if (rc) return rc;
+        graph_drop(lru);
+        lru->state = 1;
+        lru->hash = graph_hash(c, J, st);                      /* the pool as the call left it */
+        lru->plan = J->P[0];
+        lru->send = J->send[0]; lru->recv = J->recv[0]; lru->st = st; lru->pool = c->pool;
+        lru->exch = c->exch; lru->slices = c->exch_slices; lru->keep = c->keep;
+        lru->stamp = ++w->graph_clock;
+        return MPI_SUCCESS;
+    }
+    rc = graph_capture(c, J, st ? st : c->gstream, &x);       /* second sighting: capture */
+    if (rc) {
+        c->graph_error = rc;
+        graph_drop(g);
+        c->last_graph = 0;
+        return run_device_eager(c, J, st);
+    }
+    g->exec = x;
+    g->state = 2;
+    g->ran_exch = c->ran_exch;
+    g->stamp = ++w->graph_clock;
+    c->last_graph = 2;
+    return graph_launch(c, x, st);
+}
+
+int mvxi_run_device(mvx_comm_t *c, const job_t *J, hipStream_t st)
+{
+    if (graph_eligible(c, J)) return run_device_graph(c, J, st);
+    c->last_graph = 0;
+    return run_device_eager(c, J, st);
 }

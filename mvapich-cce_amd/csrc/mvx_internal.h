@@ -131,6 +131,7 @@ typedef struct {
 } job_t;
 
 MVXI int mvxi_job_kinds(job_t *J);
+MVXI void mvxi_graphs_clear(mvx_comm_t *c);
 MVXI int mvxi_run_device(mvx_comm_t *c, const job_t *J, hipStream_t st);
 MVXI int mvxi_exec_group(rank_exec_t *X, mvx_xport *t, int nr, hipStream_t st, mvx_comm_t *timed);
 MVXI size_t mvxi_region_layout(mvx_comm_t *c, rank_exec_t *X, const job_t *J, const mvx_plan *Q, size_t *off);
@@ -162,10 +163,37 @@ MVXI int mvxi_run_staged(mvx_comm_t *c, const job_t *J, hipStream_t st);
 MVXI int mvxi_typed_copy(mvx_comm_t *c, int dt, long n, const char *send, char *recv, hipStream_t st, int sync);
 MVXI void mvxi_stage_release(stage_res_t *S);
 
+/* ---- graphs of device calls (mvx_exec.c) ---------------------------------
+ * With graphs on (mvx_comm_set_graphs), a device-buffer call whose job was
+ * seen before is captured once into a HIP graph -- RCCL's transfer groups,
+ * the combine launches, the cross-stream events of PIPE -- and replayed:
+ * one hipGraphLaunch instead of the host issue of every group and kernel.
+ * The key is everything the captured work depends on: the plan, the
+ * buffers, the stream, the staging pool and the variant. */
+#define GRAPH_CACHE 16
+typedef struct {
+    int state;                  /* 0 free, 1 seen once (ran eagerly), 2 captured */
+    unsigned long long hash;
+    mvx_plan plan;
+    const char *send;
+    char *recv;
+    hipStream_t st;
+    char *pool;
+    int exch, slices, keep;
+    hipGraphExec_t exec;
+    int ran_exch;
+    unsigned long stamp;
+} graph_ent_t;
+
+/* a capture is open on this thread: staging must not be reallocated */
+extern __thread int mvxi_capturing MVXI;
+
 /* ---- communicators (mvx_comm.c) ------------------------------------------ */
 /* The tables one call works in: formerly process statics, now owned by the
  * communicator (allocated at its first call, freed with it). */
 typedef struct mvx_work {
+    graph_ent_t graphs[GRAPH_CACHE];           /* captured device calls */
+    unsigned long graph_clock;
     mvx_plan call_plan;                        /* mvx_api.c run(): this rank's plan */
     mvx_plan pipe[3][MVX_MAXP];                /* PIPE: slice plans t, t-1, t-2 */
     rank_exec_t px0[MVX_MAXP], px[3][MVX_MAXP];
@@ -211,6 +239,11 @@ struct mvx_comm_t {
     int keep;                   /* this call's (op, type) is undefined: every combine keeps its inout */
     int ran_exch;               /* the variant the last call ran (mvx_comm_last_exchange), -1 none */
     hipStream_t last_st;        /* the stream of the last call (an abort's drain check) */
+    int graphs;                 /* mvx_comm_set_graphs: capture / replay device calls */
+    int graph_error;            /* a capture failed: graphs stay off on this communicator */
+    int last_graph;             /* the last call: 0 eager, 1 replayed, 2 captured and launched */
+    hipStream_t gstream;        /* graphs of null-stream calls run here (fork / join) */
+    hipEvent_t gev[2];
     mvx_work *w;                /* per-call tables, NULL until the first call */
 };
 

@@ -138,17 +138,35 @@ static unsigned g_last_blocks;
 static size_t g_last_lds;
 static const void *g_last_fn;
 
+// LDS per CU of the device the kernels run on, from its architecture name
+// (the runtime's per-multiprocessor attribute reports the 64 KiB per-block
+// limit instead): gfx950 has 160 KiB; earlier CDNA parts 64 KiB.  A
+// reservation sized for 160 KiB on a 64 KiB part would cap the kernel at one
+// resident block per CU, so the reservation follows the part.
+static size_t lds_per_cu()
+{
+    static size_t v = 0;
+    if (v) return v;
+    int dev = 0;
+    hipDeviceProp_t pr;
+    v = 64 * 1024;
+    if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&pr, dev) == hipSuccess) {
+        if (!strncmp(pr.gcnArchName, "gfx950", 6)) v = 160 * 1024;
+    } else {
+        (void)hipGetLastError();
+    }
+    return v;
+}
+
 // dynamic LDS per block that leaves room for `cap` blocks per CU and not one
 // more (the kernels do not touch it): the middle of the range,
 // 2 * LDS / (2 * cap + 1), clear of the allocator's rounding at the edges; at
-// most 64 KiB (no function attribute needed).  gfx950: 160 KiB of LDS per CU
-// (the runtime's per-multiprocessor attribute reports the 64 KiB per-block
-// limit instead)
+// most 64 KiB (no function attribute needed).
 static size_t cap_lds(int cap)
 {
-    const size_t lds_per_cu = 160 * 1024;
+    const size_t lds = lds_per_cu();
     if (cap < 2) return 0;
-    const size_t b = (lds_per_cu * 2 / (size_t)(2 * cap + 1)) & ~(size_t)1023;
+    const size_t b = (lds * 2 / (size_t)(2 * cap + 1)) & ~(size_t)1023;
     return b > 64 * 1024 ? 64 * 1024 : b;
 }
 

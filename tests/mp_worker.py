@@ -7,7 +7,7 @@ the collectives through its libmvx.so communicator and compares its own
 result with the oracle's replay of the reference schedule
 (oracle/coll_sim.c) computed over all ranks' inputs.  Writes a JSON report.
 
-  mp_worker.py RANK WORLD PORT OUT.json TRANSPORT(host|rccl|rccl-net) SUITE(small|random|full)
+  mp_worker.py RANK WORLD PORT OUT.json TRANSPORT(host|rccl|rccl-net) SUITE(small|random|full|mixed|graph)
 
 rccl-net: RCCL communicators whose ranks may share one GPU, the bytes moved
 by RCCL's own socket transport (transport.rccl_net_env).
@@ -145,6 +145,94 @@ def main():
                       tag=name + " #%d" % i)
             else:
                 check(coll, dtype, op, n, where, root=root, tag=name + " #%d" % i)
+    elif suite == "graph":
+        # graphs on: each job three times on the same buffers -- eager,
+        # captured, replayed -- through the blocking call (the null stream:
+        # fork / join onto the communicator's stream) and the stream-ordered
+        # one on a torch stream; every result checked against the oracle
+        report["graph_states"] = {}
+        side = torch.cuda.Stream()
+        comm.set_graphs(True)
+        for name, mode, sl in modes:
+            assert comm.set_exchange(mode, sl) == 0
+            for op, dtype in [(102, 10), (111, 17), (105, 8), (103, 6)]:
+                for coll_kind, n in (("ar", 70001), ("ar", 4096 * world * 4), ("ar", 300000), ("rs", 140000),
+                                     ("red", 70001)):
+                    E = mvx.dtype_info(dtype)[0]
+                    cnts = [n] * world if coll_kind == "rs" else None
+                    tot = n * world if cnts else n
+                    S = inputs(dtype, tot, None)
+                    nrecv = n if cnts else tot
+                    R0 = [np.zeros(max(cnts[q] if cnts else tot, 1), S[0].dtype) for q in range(world)]
+                    s8, r8 = [x.view(np.uint8) for x in S], [x.view(np.uint8) for x in R0]
+                    root = world - 1
+                    if coll_kind == "ar":
+                        rref = O.allreduce(s8, r8, tot, dtype, op)
+                    elif coll_kind == "rs":
+                        rref = O.reduce_scatter(s8, r8, cnts, dtype, op)
+                    else:
+                        rref = O.reduce(s8, r8, tot, dtype, op, root)
+                    sbuf = T.to_dev(S[rank])
+                    rbuf = torch.zeros(max(nrecv, 1) * E, dtype=torch.uint8, device="cuda")
+                    for via in ("blocking", "stream"):
+                        states = []
+                        for rep in range(3):
+                            rbuf.zero_()
+                            torch.cuda.synchronize()
+                            if via == "blocking":
+                                if coll_kind == "ar":
+                                    rc = mvx.MPI_Allreduce(sbuf, rbuf, tot, dtype, op, comm)
+                                elif coll_kind == "rs":
+                                    rc = mvx.MPI_Reduce_scatter(sbuf, rbuf, cnts, dtype, op, comm)
+                                else:
+                                    rc = mvx.MPI_Reduce(sbuf, rbuf, tot, dtype, op, root, comm)
+                            else:
+                                side.wait_stream(torch.cuda.current_stream())
+                                if coll_kind == "ar":
+                                    rc = comm.allreduce_async(sbuf, rbuf, tot, dtype, op, side)
+                                elif coll_kind == "rs":
+                                    rc = comm.reduce_scatter_async(sbuf, rbuf, cnts, dtype, op, side)
+                                else:
+                                    rc = comm.reduce_async(sbuf, rbuf, tot, dtype, op, root, side)
+                                side.synchronize()
+                            states.append(comm.last_graph()[0])
+                            report["checked"] += 1
+                            ok = rc == rref[rank]
+                            if ok and rc == 0 and (coll_kind != "red" or rank == root):
+                                try:
+                                    T.assert_same(op, dtype, T.from_dev(rbuf)[: nrecv * E], R0[rank][:nrecv],
+                                                  typemap_only=True)
+                                except AssertionError as e:
+                                    ok = False
+                                    report["fails"].append([coll_kind, dtype, op, tot, via, rep, str(e)[:200]])
+                            elif not ok:
+                                report["fails"].append([coll_kind, dtype, op, tot, via, rep, rc, rref[rank]])
+                        key = "%s %s" % (name, via)
+                        report["graph_states"].setdefault(key, []).append(states)
+            report["graph_error"] = comm.last_graph()[1]
+        comm.set_graphs(False)
+    elif suite == "mixed":
+        # buffer kinds differing between the ranks of one call (MPI allows
+        # it): rank r passes host buffers when (case + r) is even, device
+        # buffers otherwise -- host calls run on HBM mirrors and move what a
+        # device call moves, so the transfers pair up
+        case = 0
+        for name, mode, sl in modes:
+            assert comm.set_exchange(mode, sl) == 0
+            for op, dtype in [(102, 10), (111, 17), (105, 8), (103, 6)]:
+                for n in (10, 70001, 300000, 4096 * world * 4):
+                    check("ar", dtype, op, n, "host" if (case + rank) % 2 == 0 else "device", tag=name)
+                    case += 1
+                for n in (5, 70001):
+                    check("red", dtype, op, n, "host" if (case + rank) % 2 == 0 else "device", root=world - 1,
+                          tag=name)
+                    case += 1
+                for base in (3, 140000):
+                    check("rs", dtype, op, [base] * world, "host" if (case + rank) % 2 == 0 else "device",
+                          tag=name)
+                    case += 1
+                check("scan", dtype, op, 5000, "host" if (case + rank) % 2 == 0 else "device", tag=name)
+                case += 1
     else:
         # the BASELINE multi-GPU shapes at full size: C3, C4 (p = 4 in the
         # config; any p here), C5

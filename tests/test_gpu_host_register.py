@@ -1,0 +1,131 @@
+"""GPU: the registration cache for pageable host buffers (mvx_host.c;
+MVAPICH's dreg, mpid/ch_gen2/dreg.c:774-832).
+
+With the cache on, a pageable range a call uses is page-locked on first use
+and found again on later calls (hits), so those DMA directly.  A registered
+buffer that is freed and reallocated at the same size must still reduce
+bit-exact: with mvx_host_unregister before the free (the contract), and --
+recorded separately -- without it.  Results are checked against numpy (sums
+of small integers in float32 are exact) and the oracle's MPIR_SUM.
+"""
+import ctypes
+import importlib
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+MIB = 1 << 20
+
+
+@pytest.fixture()
+def mvx():
+    m = importlib.import_module("mvapich-cce_amd")
+    m.host_register_enable(True)
+    yield m
+    m.host_register_enable(False)
+
+
+def _libc_buffer(nbytes):
+    """malloc'd memory (mmap'd at this size: free() unmaps it, the next
+    malloc of the same size usually maps the same range again)"""
+    libc = ctypes.CDLL("libc.so.6")
+    libc.malloc.restype = ctypes.c_void_p
+    libc.malloc.argtypes = [ctypes.c_size_t]
+    libc.free.argtypes = [ctypes.c_void_p]
+    p = libc.malloc(nbytes)
+    assert p
+    return libc, p
+
+
+def _as_array(p, n):
+    return np.ctypeslib.as_array((ctypes.c_float * n).from_address(p))
+
+
+def _sum_call(mvx, x, y, n):
+    mvx.MPIR_call("MPIR_SUM", x, y, n, mvx.MPI_FLOAT)
+    assert mvx.op_errno() == 0
+
+
+@pytest.mark.parametrize("mib", [2, 80])
+def test_repeat_calls_hit_the_cache(mvx, mib):
+    """the first call registers both operands, later calls find them"""
+    n = mib * MIB // 4
+    rng = np.random.default_rng(mib)
+    a = rng.integers(-8, 8, n).astype(np.float32)
+    b = rng.integers(-8, 8, n).astype(np.float32)
+    want = a + b
+    s0 = mvx.host_register_stats()
+    for rep in range(3):
+        y = b.copy() if rep == 0 else y
+        if rep:
+            np.copyto(y, b)
+        _sum_call(mvx, a, y, n)
+        assert np.array_equal(y, want), rep
+    s1 = mvx.host_register_stats()
+    assert s1["entries"] >= 2 and s1["misses"] - s0["misses"] == 2, (s0, s1)
+    assert s1["hits"] - s0["hits"] >= 4, (s0, s1)
+    assert mvx.host_unregister(a) == 0 and mvx.host_unregister(y) == 0
+    assert mvx.host_unregister(a) != 0          # nothing left at that address
+
+
+@pytest.mark.parametrize("unregister", [True, False])
+def test_free_and_reallocate_same_size(mvx, unregister):
+    """A registered buffer is freed and the same size allocated again (the
+    same address in practice); the call on the new buffer must see its new
+    contents.  unregister=True is the documented contract; False records
+    what the driver does without it."""
+    n = 96 * MIB // 4
+    libc, px = _libc_buffer(n * 4)
+    _, py = _libc_buffer(n * 4)
+    x, y = _as_array(px, n), _as_array(py, n)
+    x[:] = 1.0
+    y[:] = 2.0
+    _sum_call(mvx, px, py, n)
+    assert np.all(y == 3.0)
+    if unregister:
+        assert mvx.host_unregister(px) == 0 and mvx.host_unregister(py) == 0
+    libc.free(px)
+    libc.free(py)
+    qx = _libc_buffer(n * 4)[1]
+    qy = _libc_buffer(n * 4)[1]
+    x2, y2 = _as_array(qx, n), _as_array(qy, n)
+    rng = np.random.default_rng(7)
+    x2[:] = rng.integers(-8, 8, n).astype(np.float32)
+    y2[:] = rng.integers(-8, 8, n).astype(np.float32)
+    want = x2 + y2
+    _sum_call(mvx, qx, qy, n)
+    same = (qx == px, qy == py)
+    ok = bool(np.array_equal(y2, want))
+    mvx.host_unregister(qx)
+    mvx.host_unregister(qy)
+    libc.free(qx)
+    libc.free(qy)
+    assert ok, "reallocated buffers (same address: %s) reduced stale data" % (same,)
+
+
+def test_cache_off_leaves_pageable_path(mvx):
+    """turned off, nothing is registered and results are unchanged"""
+    mvx.host_register_enable(False)
+    n = 70 * MIB // 4
+    a = np.full(n, 1.5, np.float32)
+    b = np.full(n, 2.0, np.float32)
+    _sum_call(mvx, a, b, n)
+    assert np.all(b == 3.5)
+    assert mvx.host_register_stats()["entries"] == 0
+
+
+def test_partial_overlap_is_widened(mvx):
+    """a call on a longer range than the one registered replaces the
+    registration with the union (no DMA past pinned pages)"""
+    n = 64 * MIB // 4
+    a = np.ones(2 * n, np.float32)
+    b = np.ones(2 * n, np.float32)
+    _sum_call(mvx, a[:n], b[:n], n)
+    assert np.all(b[:n] == 2.0) and np.all(b[n:] == 1.0)
+    _sum_call(mvx, a, b, 2 * n)
+    assert np.all(b[:n] == 3.0) and np.all(b[n:] == 2.0)
+    st = mvx.host_register_stats()
+    assert st["bytes"] >= 2 * (2 * n * 4), st
+    mvx.host_unregister(a)
+    mvx.host_unregister(b)

@@ -126,6 +126,41 @@ def test_rccl_multirank_net_transport(world):
                 assert ran["pipe"].get("1", 0) > 0, ran
 
 
+@pytest.mark.parametrize("world,transport", [(2, "host"), (3, "host"), (2, "rccl-net"), (4, "rccl-net")])
+def test_mixed_buffer_kinds_across_ranks(world, transport):
+    """One call, different buffer kinds on different ranks (host on some,
+    device on others -- legal MPI): the host ranks run on HBM mirrors and
+    their transfers pair with the device ranks' under every exchange
+    variant; every rank bit-exact against the oracle's replay."""
+    for rep in _launch(world, transport, "mixed", 600):
+        assert rep["checked"] > 50
+        assert not rep["fails"], rep["fails"][:5]
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_graphs_rccl_net(world):
+    """HIP graphs of RCCL device calls (mvx_comm_set_graphs) on RCCL
+    communicators sharing the GPU: every job eager, then captured, then
+    replayed -- on the null stream (fork / join) and on a torch stream --
+    under P2P, PIPE and COLL; every result bit-exact against the oracle."""
+    for rep in _launch(world, "rccl-net", "graph", 600):
+        assert rep["checked"] > 100
+        assert not rep["fails"], rep["fails"][:5]
+        assert rep["graph_error"] == 0, rep["graph_error"]
+        for key, runs in rep["graph_states"].items():
+            for states in runs:
+                # a job that moves nothing between ranks runs eagerly
+                assert states in ([0, 2, 1], [0, 0, 0]), (key, states)
+            assert any(st == [0, 2, 1] for st in runs), (key, runs)
+
+
+def test_graphs_host_transport_stay_eager():
+    """a caller-supplied transport (host callbacks) is never captured"""
+    for rep in _launch(2, "host", "graph", 600):
+        assert not rep["fails"], rep["fails"][:5]
+        assert all(st == [0, 0, 0] for runs in rep["graph_states"].values() for st in runs)
+
+
 def _bench_host(cfg, extra_env=None, world=2, transport="host", extra_args=()):
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
     env.update(extra_env or {})
@@ -192,6 +227,10 @@ def test_bench_multi_gpu_leg_rccl_net(cfg):
     assert all(v["parity"] for v in tuning.values()), tuning
     assert tuning["coll"]["ran"] == "coll" and tuning["p2p"]["ran"] == "p2p", tuning
     assert all(v["host_issue_us"] > 0 for v in tuning.values()), tuning
+    # the graph variants: RCCL's groups captured into HIP graphs and replayed
+    for name in ("p2p+g", "pipe+g", "pipe8+g", "coll+g"):
+        assert tuning[name]["graph"] == {"state": "replayed", "capture_error": 0}, (name, tuning[name])
+        assert tuning[name]["ran"] == tuning[name.split("+")[0]]["ran"], tuning
     # RCCL's own reduction on the same communicator, timed after the line
     nat = d["rccl_native"]
     assert nat["op"] == ("ncclAllReduce(ncclSum)" if cfg == "c3" else "ncclReduceScatter(ncclSum)"), nat
@@ -218,7 +257,10 @@ def test_bench_full_size_eight_ranks_rccl_net():
     assert d["parity"] == "bit-exact vs the reference schedule, all 8 ranks", d["parity"]
     tuning = d["config"]["exchange_tuning"]
     for name, v in tuning.items():
-        assert v["parity"] and v["ran"] == ("coll" if name == "coll" else name[:4]), (name, v)
+        base = name.split("+")[0]
+        assert v["parity"] and v["ran"] == ("coll" if base == "coll" else base[:4]), (name, v)
+        if name.endswith("+g"):
+            assert v["graph"]["state"] == "replayed", (name, v)
     (o,) = d["other_configs"]
     assert o["config"] == "c5" and o["vector_bytes_per_rank"] == 512 << 20
     assert o["parity"] == "bit-exact vs the reference schedule, all 8 ranks", o
@@ -265,8 +307,9 @@ def test_bench_survives_a_failing_variant(bad):
 
 def test_bench_no_clean_variant_exits_nonzero():
     """Every variant failing: no throughput line, a nonzero exit."""
-    p = _bench_host("c3", {"MVX_BENCH_FAIL": ",".join("%s@1" % v for v in
-                                                      ("p2p", "pipe", "pipe2", "pipe8", "coll"))})
+    sys.path.insert(0, ROOT)
+    import bench
+    p = _bench_host("c3", {"MVX_BENCH_FAIL": ",".join("%s@1" % v for v in bench.EXCH)})
     assert p.returncode != 0
     assert not [x for x in p.stdout.splitlines() if x.startswith("{")]
 
@@ -339,8 +382,9 @@ def test_bench_self_launch_driver_form(transport):
 def test_bench_self_launch_worker_failure_exits_nonzero():
     """Workers that end without a line take the job down: the launcher exits
     with their worst code and prints no line (every variant fails on rank 1)."""
-    p = _bench_self(2, "host", extra_env={"MVX_BENCH_FAIL": ",".join(
-        "%s@1" % v for v in ("p2p", "pipe", "pipe2", "pipe8", "coll"))})
+    sys.path.insert(0, ROOT)
+    import bench
+    p = _bench_self(2, "host", extra_env={"MVX_BENCH_FAIL": ",".join("%s@1" % v for v in bench.EXCH)})
     assert p.returncode != 0
     assert not [x for x in p.stdout.splitlines() if x.startswith("{")]
 

@@ -15,6 +15,9 @@ PCIe (H2D in, D2H out).  For float32 vectors of 8 B ... 256 MiB, one line per
   ar1_pinned    the same on pinned host buffers (DMA straight from them)
   ar4_local_*   a 4-rank virtual communicator (one process, loopback), the
                 sum of 4 vectors: host buffers staged per rank
+  *_registered  pageable numpy arrays with the registration cache on
+                (mvx_host_register_enable): the first call page-locks them
+                ("first_us"), the timed calls DMA them directly
 
 Every result is checked against numpy (float32 sums of small integers are
 exact).  usage: bench_host.py [--min-mib M] [--max-mib 256] [--cases a,b,...]
@@ -29,13 +32,14 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 MIB, GIB = 1 << 20, 1 << 30
-ALL = ["op_device", "op_pageable", "op_pinned", "ar1_device", "ar1_pageable", "ar1_pinned",
-       "ar4_local_device", "ar4_local_pageable"]
+ALL = ["op_device", "op_pageable", "op_pinned", "op_registered", "ar1_device", "ar1_pageable", "ar1_pinned",
+       "ar1_registered", "ar4_local_device", "ar4_local_pageable"]
 
 
-def timeit(fn, budget=0.25, max_reps=2000):
+def timeit(fn, budget=0.25, max_reps=2000, warm=True):
     """median seconds of fn over as many calls as fit in `budget` (>= 3)"""
-    fn()
+    if warm:
+        fn()
     ts = []
     t_end = time.perf_counter() + budget
     while len(ts) < 3 or (time.perf_counter() < t_end and len(ts) < max_reps):
@@ -80,6 +84,8 @@ def main():
         b0 = rng.integers(-8, 8, n).astype(np.float32)
         want = a + b0
         for case in cases:
+            first = None
+            mvx.host_register_enable(case.endswith("_registered"))
             if case.startswith("op_"):
                 where = case[3:]
                 if where == "device":
@@ -94,14 +100,16 @@ def main():
                     y.copy_(y0) if torch.is_tensor(y) else np.copyto(y, y0)
                     mvx.MPIR_call("MPIR_SUM", x, y, n, F)
 
+                t0 = time.perf_counter()
                 call()
+                first = time.perf_counter() - t0
                 got = y.cpu().numpy() if torch.is_tensor(y) else y
                 assert mvx.op_errno() == 0 and np.array_equal(got, want), case
 
                 def fn():
                     mvx.MPIR_call("MPIR_SUM", x, y, n, F)
                 t, reps = timeit(fn)
-                pcie = {"device": 0, "pinned": 3, "pageable": 3}[where] * nbytes
+                pcie = {"device": 0, "pinned": 3, "pageable": 3, "registered": 3}[where] * nbytes
             elif case.startswith("ar1_"):
                 where = case[4:]
                 if where == "device":
@@ -113,7 +121,9 @@ def main():
 
                 def fn():
                     assert mvx.MPI_Allreduce(x, y, n, F, SUM, comm) == 0
+                t0 = time.perf_counter()
                 fn()
+                first = time.perf_counter() - t0
                 got = y.cpu().numpy() if torch.is_tensor(y) else y
                 assert np.array_equal(got, a), case
                 t, reps = timeit(fn)
@@ -139,7 +149,11 @@ def main():
                 t, reps = timeit(fn)
                 pcie = 0 if where == "device" else 8 * nbytes
                 del xs, ys
+            reg = mvx.host_register_stats()
+            mvx.host_register_enable(False)          # drops every registration
             print(json.dumps({"case": case, "bytes": nbytes, "us": round(t * 1e6, 2), "reps": reps,
+                              "first_us": round(first * 1e6, 2) if first is not None else None,
+                              "registered": reg if case.endswith("_registered") else None,
                               "GiB_per_s_per_vector": round(nbytes / t / GIB, 3),
                               "pcie_bytes": pcie, "pcie_GBps": round(pcie / t / 1e9, 2) if pcie else None}),
                   flush=True)
