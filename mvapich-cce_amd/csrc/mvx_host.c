@@ -21,9 +21,13 @@
  * MVX_HOST_REGISTER_MIN_KIB (default 1024) are never registered.  The
  * reference learns of freed memory through malloc hooks (mem_hooks.c); here
  * the contract is mvx_host_unregister(addr) before the memory is freed.
- * (What the driver does when a registered range is unmapped and mapped
- * again without the call is measured, not assumed: DESIGN.md section 5a,
- * tests/test_gpu_host_register.py.)
+ * The contract is not optional: on MI355X a registered range that is freed
+ * (unmapped) and handed out again by malloc at the same address, with no
+ * mvx_host_unregister in between, left the GPU in the memory-access-fault
+ * state at its next DMA (round 4).  No CPU-side check
+ * sees the free, and a probing DMA would fault the same way; that is why
+ * the cache is off unless the application asks for it and keeps the
+ * contract.
  */
 #include <pthread.h>
 #include <stdint.h>
@@ -237,6 +241,7 @@ int mvx_host_unregister(const void *addr)
 int mvx_host_register_stats(long *entries, size_t *bytes, long *hits, long *misses)
 {
     pthread_mutex_lock(&g_reg.mu);
+    reg_env();
     if (entries) *entries = g_reg.n;
     if (bytes) *bytes = g_reg.total;
     if (hits) *hits = (long)g_reg.hits;
