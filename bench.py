@@ -906,7 +906,10 @@ def run_multi(args, mvx, dev, world, rank, local, clock):
     n = nbytes // E
     n -= n % world
     nbytes = n * E
-    stream = torch.cuda.current_stream()
+    # a stream of its own (not the null stream): graph variants launch on it
+    # directly instead of forking from and joining back to the null stream
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
     tp = importlib.import_module("mvapich-cce_amd.transport") if args.transport == "host" else None
 
     def new_comm():

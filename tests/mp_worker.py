@@ -22,6 +22,8 @@ sys.path[:0] = [ROOT, HERE]
 
 
 def main():
+    import faulthandler
+    faulthandler.enable()           # a crash in native code names the Python line it came from
     rank, world, port, out, transport, suite = (int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4],
                                                  sys.argv[5], sys.argv[6])
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
@@ -177,6 +179,10 @@ def main():
                     for via in ("blocking", "stream"):
                         states = []
                         for rep in range(3):
+                            if os.environ.get("MVX_MP_TRACE"):
+                                sys.stderr.write("rank %d: %s %s op %d type %d n %d %s rep %d\n"
+                                                 % (rank, name, coll_kind, op, dtype, n, via, rep))
+                                sys.stderr.flush()
                             rbuf.zero_()
                             torch.cuda.synchronize()
                             if via == "blocking":

@@ -1,7 +1,7 @@
 """GPU: the executor around the kernels.
 
 * Host buffers (MPI user buffers live in host memory, allreduce.c:57-92):
-  the staged pipeline slices every rank's plan (mvx_coll.c plan_slice) and
+  the staged pipeline slices every rank's plan (mvx_exec.c mvxi_plan_slice) and
   overlaps host copies, H2D, the collective and D2H.  Pageable, page-locked
   and mixed host/device buffers, several slices per call, against the
   oracle's replay of the reference schedule.

@@ -33,7 +33,7 @@ def run(mvx, name, op, dtype, k, shape, leaf_bytes, sets, reps=20, warm=3, quiet
     for s in range(sets):
         if k > 2:
             # the executor's staging pool: shard slots back to back, 4 KiB
-            # staggered (mvx_coll.c exec_layout)
+            # staggered (mvx_exec.c exec_layout)
             big = torch.randint(0, 1 << 30, (k * (leaf_bytes + 4096) // 4,), dtype=torch.int32, device="cuda")
             leaves = [big[q * (leaf_bytes + 4096) // 4:][: leaf_bytes // 4] for q in range(k)]
         else:
