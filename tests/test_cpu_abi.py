@@ -128,3 +128,29 @@ def test_plan_phase_ranges_are_consistent(mvx):
                                 assert P[r].b_send[s].off == P[s].b_recv[r].off
                             if P[r].a_recv[s].cnt:
                                 assert (P[r].a_recv[s].off, P[r].a_recv[s].cnt) == (P[r].c_src_off, P[r].c_cnt)
+
+
+def test_transport_table_is_read_only_as_far_as_the_caller_says(mvx):
+    """mvx_comm_init_transport_ex reads `bytes` of the table: below the base
+    (ctx + the four phase callbacks) it is an argument error, whatever the
+    rest holds; a table with no callbacks is refused before any device call."""
+    tp = __import__("importlib").import_module("mvapich-cce_amd.transport")
+    h = ctypes.c_int()
+    t = tp.Transport()
+    L = mvx.coll()
+    base = ctypes.sizeof(t) - 2 * ctypes.sizeof(ctypes.c_void_p)
+    assert L.mvx_comm_init_transport_ex(ctypes.byref(h), 0, 2, 0, ctypes.byref(t), base - 1) == mvx.MPI_ERR_ARG
+    assert L.mvx_comm_init_transport_ex(ctypes.byref(h), 0, 2, 0, ctypes.byref(t), ctypes.sizeof(t)) == mvx.MPI_ERR_ARG
+    assert L.mvx_comm_init_transport(ctypes.byref(h), 0, 2, 0, ctypes.byref(t)) == mvx.MPI_ERR_ARG
+
+
+def test_comm_knob_entry_points_reject_null_communicators(mvx):
+    L = mvx.coll()
+    code = 197                    # MPI_ERR_COMM | 3 << 6, as the reference's null-comm test
+    st, err = ctypes.c_int(), ctypes.c_int()
+    assert L.mvx_comm_set_graphs(12345, 1) == code
+    assert L.mvx_comm_last_graph(12345, ctypes.byref(st), ctypes.byref(err)) == code
+    assert L.mvx_comm_set_host_pipeline(12345, 1) == code
+    assert L.mvx_comm_rccl_info(12345, None, None, None) == code
+    assert L.mvx_comm_reap() == 0            # nothing parked in this process
+    assert L.mvx_host_unregister(ctypes.c_void_p(4096)) != 0
