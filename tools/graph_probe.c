@@ -1,0 +1,133 @@
+/*
+ * graph_probe.c -- does RCCL's grouped send / receive survive HIP stream
+ * capture, instantiation and replay here?  Two processes (forked before any
+ * HIP call) share the box's one GPU as two "hosts" (NCCL_HOSTID, RCCL's
+ * socket transport, as transport.rccl_net_env), exchange a buffer eagerly,
+ * then capture the same exchange into a graph, launch it three times and
+ * check the bytes after each launch.  Prints one line per step, so a crash
+ * names the step it happened in.
+ *
+ *   gcc -O2 -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include tools/graph_probe.c \
+ *       -o tools/graph_probe -L/opt/rocm/lib -lrccl -lamdhip64
+ */
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/wait.h>
+#include <unistd.h>
+
+#include <hip/hip_runtime_api.h>
+#include <rccl/rccl.h>
+
+#define N (1 << 20)
+#define CHK(x, what)                                                               \
+    do {                                                                           \
+        if (!(x)) {                                                                \
+            fprintf(stderr, "rank %d: %s failed\n", rank, what);                   \
+            return 1;                                                              \
+        }                                                                          \
+    } while (0)
+
+static int step(int rank, const char *s)
+{
+    fprintf(stderr, "rank %d: %s\n", rank, s);
+    return 0;
+}
+
+static int exchange(ncclComm_t comm, int rank, const int *send, int *recv, hipStream_t st)
+{
+    if (ncclGroupStart() != ncclSuccess) return 1;
+    if (ncclSend(send, N, ncclInt32, 1 - rank, comm, st) != ncclSuccess) return 1;
+    if (ncclRecv(recv, N, ncclInt32, 1 - rank, comm, st) != ncclSuccess) return 1;
+    return ncclGroupEnd() != ncclSuccess;
+}
+
+static int check(int rank, int *recv, int *host, int tag)
+{
+    int i;
+    if (hipMemcpy(host, recv, N * sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return 1;
+    for (i = 0; i < N; i++)
+        if (host[i] != (1 - rank) * 1000003 + i) {
+            fprintf(stderr, "rank %d: %d: recv[%d] = %d\n", rank, tag, i, host[i]);
+            return 1;
+        }
+    return 0;
+}
+
+static int run(int rank, ncclUniqueId id)
+{
+    char hid[32];
+    ncclComm_t comm;
+    hipStream_t st;
+    hipGraph_t g;
+    hipGraphExec_t x;
+    int *send, *recv, *host, i;
+    snprintf(hid, sizeof hid, "probe-rank-%d", rank);
+    setenv("NCCL_HOSTID", hid, 1);
+    CHK(hipSetDevice(0) == hipSuccess, "hipSetDevice");
+    CHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess, "stream");
+    CHK(hipMalloc((void **)&send, N * sizeof(int)) == hipSuccess, "malloc");
+    CHK(hipMalloc((void **)&recv, N * sizeof(int)) == hipSuccess, "malloc");
+    host = (int *)malloc(N * sizeof(int));
+    for (i = 0; i < N; i++) host[i] = rank * 1000003 + i;
+    CHK(hipMemcpy(send, host, N * sizeof(int), hipMemcpyHostToDevice) == hipSuccess, "h2d");
+    step(rank, "init");
+    CHK(ncclCommInitRank(&comm, 2, id, rank) == ncclSuccess, "ncclCommInitRank");
+    step(rank, "eager exchange");
+    CHK(exchange(comm, rank, send, recv, st) == 0, "eager exchange");
+    CHK(hipStreamSynchronize(st) == hipSuccess, "eager sync");
+    CHK(check(rank, recv, host, -1) == 0, "eager result");
+    step(rank, "capture");
+    CHK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal) == hipSuccess, "begin capture");
+    CHK(hipMemsetAsync(recv, 0, N * sizeof(int), st) == hipSuccess, "memset in capture");
+    CHK(exchange(comm, rank, send, recv, st) == 0, "captured exchange");
+    CHK(hipStreamEndCapture(st, &g) == hipSuccess, "end capture");
+    step(rank, "instantiate");
+    CHK(hipGraphInstantiate(&x, g, NULL, NULL, 0) == hipSuccess, "instantiate");
+    for (i = 0; i < 3; i++) {
+        step(rank, "launch");
+        CHK(hipGraphLaunch(x, st) == hipSuccess, "launch");
+        CHK(hipStreamSynchronize(st) == hipSuccess, "launch sync");
+        CHK(check(rank, recv, host, i) == 0, "replayed result");
+    }
+    step(rank, "ok");
+    hipGraphExecDestroy(x);
+    hipGraphDestroy(g);
+    ncclCommDestroy(comm);
+    return 0;
+}
+
+int main(void)
+{
+    ncclUniqueId id;
+    int fd[2], r, rc = 0, status;
+    pid_t kid[2];
+    setenv("NCCL_SOCKET_IFNAME", "lo", 0);
+    setenv("NCCL_IB_DISABLE", "1", 0);
+    /* the id is made by a child too: nothing in this parent touches HIP */
+    if (pipe(fd)) return 1;
+    kid[0] = fork();
+    if (kid[0] == 0) {
+        close(fd[0]);
+        if (ncclGetUniqueId(&id) != ncclSuccess) _exit(1);
+        if (write(fd[1], &id, sizeof id) != sizeof id) _exit(1);
+        _exit(0);
+    }
+    close(fd[1]);
+    if (read(fd[0], &id, sizeof id) != sizeof id) return 1;
+    waitpid(kid[0], &status, 0);
+    for (r = 0; r < 2; r++) {
+        kid[r] = fork();
+        if (kid[r] == 0) _exit(run(r, id));
+    }
+    for (r = 0; r < 2; r++) {
+        waitpid(kid[r], &status, 0);
+        if (!WIFEXITED(status) || WEXITSTATUS(status)) {
+            fprintf(stderr, "rank %d: %s %d\n", r, WIFSIGNALED(status) ? "signal" : "exit",
+                    WIFSIGNALED(status) ? WTERMSIG(status) : WEXITSTATUS(status));
+            rc = 1;
+        }
+    }
+    printf("graph_probe: %s\n", rc ? "FAILED" : "ok");
+    return rc;
+}
