@@ -130,7 +130,6 @@ static int g_generic_only = 0;   // MVX_PROG_GENERIC=1: no fixed-tree kernels (A
 // as many as registers allow); MVX_CAP_{APPLY,PROG,TREE} override for A/B runs
 static int g_cap[FAM_N] = {0, 0, 2};
 static int g_no_body = 0;        // MVX_NO_BODY=1: fixed trees through k_combine (A/B runs)
-static int g_body_full = 1;      // MVX_BODY_FULL=0: the body kernels' bounds-tested loop always (A/B runs)
 static size_t g_cap_lds[FAM_N];
 static const char *g_last = "";
 static char g_last_buf[96];
@@ -186,8 +185,6 @@ static void init_env()
     if (e && atoi(e) == 1) g_generic_only = 1;
     e = getenv("MVX_NO_BODY");
     if (e && atoi(e) == 1) g_no_body = 1;
-    e = getenv("MVX_BODY_FULL");
-    if (e && atoi(e) == 0) g_body_full = 0;
     const char *caps[FAM_N] = {"MVX_CAP_APPLY", "MVX_CAP_PROG", "MVX_CAP_TREE"};
     for (int f = 0; f < FAM_N; ++f) {
         e = getenv(caps[f]);
@@ -233,8 +230,6 @@ static int launch(const KSet *ks, const KFam &F, Params &P, hipStream_t stream)
         for (int q = 0; q < P.k; ++q) B.src[q] = reinterpret_cast<const u32x4 *>(P.src[q]);
         B.dst = reinterpret_cast<u32x4 *>(P.dst);
         B.nvec = P.nvec;
-        // whole iterations only (MVX_BODY_FULL=0 forces the tested loop, A/B runs)
-        B.full = g_body_full && P.nvec % (256L * F.body_unroll) == 0;
         long work = (P.nvec * F.body_units + F.body_unroll * 256 - 1) / (F.body_unroll * 256);
         const unsigned blocks = (unsigned)(work < g_block_cap ? work : g_block_cap);
         void *bargs[] = {&B};

@@ -471,7 +471,6 @@ struct BodyParams {
     const u32x4 *src[8];
     u32x4 *dst;
     long nvec;   // chunks
-    int full;    // nvec is a whole number of iterations (256 * U chunks): no per-chunk bounds tests
 };
 
 // 56 KiB of static LDS per block: 2 resident blocks (8 waves) per CU.
@@ -486,15 +485,12 @@ struct BodyParams {
 #define BODY_ST_NT 1   // non-temporal result stores (cached: C4 204.8 -> 215.0 us, C5 96.1 -> 97.1, C3 unchanged)
 #endif
 
-// FULL: every iteration's U chunks exist (P.full: nvec a multiple of 256 * U,
-// so c0 < nvec implies c0 + 256 (U - 1) < nvec).  Without the per-chunk
-// tests the U * KMAX loads issue unconditionally and the compiler counts
-// them exactly (s_waitcnt vmcnt(n) per operand pair), where the tested form
-// must assume the smaller batch and waits for every load of the iteration
-// before its first tree step completes.
-template <int O, typename T, int KMAX, int U, bool FULL>
-__device__ __forceinline__ void tree_body_loop(const BodyParams &P)
+template <int O, typename T, int KMAX, int U>
+__global__ void __launch_bounds__(256)
+k_tree_body(const BodyParams P)
 {
+    __shared__ char lds_cap[BODY_LDS_CAP];
+    if (P.nvec < 0) lds_cap[threadIdx.x] = 0;
     constexpr int V = CG<T>::v;
     const long nthr = (long)gridDim.x * 256;
     for (long c0 = (long)blockIdx.x * (256 * U) + threadIdx.x; c0 < P.nvec; c0 += nthr * U) {
@@ -502,14 +498,14 @@ __device__ __forceinline__ void tree_body_loop(const BodyParams &P)
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const long c = c0 + (long)u * 256;
-            if (FULL || c < P.nvec)
+            if (c < P.nvec)
 #pragma unroll
                 for (int q = 0; q < KMAX; ++q) x[u][q] = ld_chunk<T, 1>(P.src[q], c);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const long c = c0 + (long)u * 256;
-            if (FULL || c < P.nvec) {
+            if (c < P.nvec) {
 #pragma unroll
                 for (int h = 1; h < KMAX; h <<= 1)
 #pragma unroll
@@ -522,21 +518,14 @@ __device__ __forceinline__ void tree_body_loop(const BodyParams &P)
     }
 }
 
+// The same over a full CHAIN ((y0 op y1) op y2) ..., the pairwise
+// Reduce_scatter's order (C4: k = 4, p = 4)
 template <int O, typename T, int KMAX, int U>
 __global__ void __launch_bounds__(256)
-k_tree_body(const BodyParams P)
+k_chain_body(const BodyParams P)
 {
     __shared__ char lds_cap[BODY_LDS_CAP];
     if (P.nvec < 0) lds_cap[threadIdx.x] = 0;
-    if (P.full) tree_body_loop<O, T, KMAX, U, true>(P);
-    else tree_body_loop<O, T, KMAX, U, false>(P);
-}
-
-// The same over a full CHAIN ((y0 op y1) op y2) ..., the pairwise
-// Reduce_scatter's order (C4: k = 4, p = 4)
-template <int O, typename T, int KMAX, int U, bool FULL>
-__device__ __forceinline__ void chain_body_loop(const BodyParams &P)
-{
     constexpr int V = CG<T>::v;
     const long nthr = (long)gridDim.x * 256;
     for (long c0 = (long)blockIdx.x * (256 * U) + threadIdx.x; c0 < P.nvec; c0 += nthr * U) {
@@ -544,14 +533,14 @@ __device__ __forceinline__ void chain_body_loop(const BodyParams &P)
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const long c = c0 + (long)u * 256;
-            if (FULL || c < P.nvec)
+            if (c < P.nvec)
 #pragma unroll
                 for (int q = 0; q < KMAX; ++q) x[u][q] = ld_chunk<T, 1>(P.src[q], c);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const long c = c0 + (long)u * 256;
-            if (FULL || c < P.nvec) {
+            if (c < P.nvec) {
 #pragma unroll
                 for (int q = 1; q < KMAX; ++q)
 #pragma unroll
@@ -560,16 +549,6 @@ __device__ __forceinline__ void chain_body_loop(const BodyParams &P)
             }
         }
     }
-}
-
-template <int O, typename T, int KMAX, int U>
-__global__ void __launch_bounds__(256)
-k_chain_body(const BodyParams P)
-{
-    __shared__ char lds_cap[BODY_LDS_CAP];
-    if (P.nvec < 0) lds_cap[threadIdx.x] = 0;
-    if (P.full) chain_body_loop<O, T, KMAX, U, true>(P);
-    else chain_body_loop<O, T, KMAX, U, false>(P);
 }
 
 // MPI_LONG_DOUBLE_INT MAXLOC / MINLOC (global_ops.c:1365-1378 / 1605-1618)

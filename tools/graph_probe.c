@@ -56,14 +56,11 @@ static int check(int rank, int *recv, int *host, int tag)
 
 static int run(int rank, ncclUniqueId id)
 {
-    char hid[32];
     ncclComm_t comm;
     hipStream_t st;
     hipGraph_t g;
     hipGraphExec_t x;
     int *send, *recv, *host, i;
-    snprintf(hid, sizeof hid, "probe-rank-%d", rank);
-    setenv("NCCL_HOSTID", hid, 1);
     CHK(hipSetDevice(0) == hipSuccess, "hipSetDevice");
     CHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess, "stream");
     CHK(hipMalloc((void **)&send, N * sizeof(int)) == hipSuccess, "malloc");
@@ -104,22 +101,28 @@ int main(void)
     pid_t kid[2];
     setenv("NCCL_SOCKET_IFNAME", "lo", 0);
     setenv("NCCL_IB_DISABLE", "1", 0);
-    /* the id is made by a child too: nothing in this parent touches HIP */
+    /* rank 0 makes the id (its process hosts RCCL's bootstrap root) and
+     * passes it to rank 1; nothing in this parent touches HIP */
     if (pipe(fd)) return 1;
-    kid[0] = fork();
-    if (kid[0] == 0) {
-        close(fd[0]);
-        if (ncclGetUniqueId(&id) != ncclSuccess) _exit(1);
-        if (write(fd[1], &id, sizeof id) != sizeof id) _exit(1);
-        _exit(0);
-    }
-    close(fd[1]);
-    if (read(fd[0], &id, sizeof id) != sizeof id) return 1;
-    waitpid(kid[0], &status, 0);
     for (r = 0; r < 2; r++) {
         kid[r] = fork();
-        if (kid[r] == 0) _exit(run(r, id));
+        if (kid[r] == 0) {
+            char hid[32];
+            snprintf(hid, sizeof hid, "probe-rank-%d", r);
+            setenv("NCCL_HOSTID", hid, 1);       /* before this process's first RCCL call */
+            if (r == 0) {
+                close(fd[0]);
+                if (ncclGetUniqueId(&id) != ncclSuccess) _exit(1);
+                if (write(fd[1], &id, sizeof id) != sizeof id) _exit(1);
+            } else {
+                close(fd[1]);
+                if (read(fd[0], &id, sizeof id) != sizeof id) _exit(1);
+            }
+            _exit(run(r, id));
+        }
     }
+    close(fd[0]);
+    close(fd[1]);
     for (r = 0; r < 2; r++) {
         waitpid(kid[r], &status, 0);
         if (!WIFEXITED(status) || WEXITSTATUS(status)) {
