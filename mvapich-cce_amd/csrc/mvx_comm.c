@@ -367,6 +367,15 @@ static int comm_release(MPI_Comm *comm, int abort)
     mvx_comm_t *c = comm ? mvxi_get_comm(*comm) : NULL;
     int i;
     if (!c) return ERR_COMM_NULL_CODE;
+    /* the graphs first: a captured RCCL group holds a reference on its
+     * communicator, and ncclCommDestroy waits for every such reference to go
+     * (measured: destroying the communicator first never returned).  An
+     * aborted communicator's graphs may still be running: left to the
+     * process, like any work queued behind its transfers. */
+    if (!abort) {
+        if (c->last_st || c->gstream) hipDeviceSynchronize();
+        mvxi_graphs_clear(c);
+    }
     if (c->nccl) {
         if (abort) ncclCommAbort(c->nccl);
         else ncclCommDestroy(c->nccl);
@@ -381,9 +390,6 @@ static int comm_release(MPI_Comm *comm, int abort)
         if (c->xpool) hipFree(c->xpool);
         if (c->w) mvxi_stage_release(&c->w->stage);
     }
-    /* an aborted communicator's graphs may still be running: left to the
-     * process, like any work queued behind its transfers */
-    if (!abort) mvxi_graphs_clear(c);
     if (c->gstream) {
         hipStreamDestroy(c->gstream);
         hipEventDestroy(c->gev[0]);

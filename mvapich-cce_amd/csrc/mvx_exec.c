@@ -7,9 +7,13 @@
  * intra_Reduce / intra_Reduce_scatter (intra_fns_new.c), as planned by
  * mvx_plan.c.
  */
+#include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "mvx_internal.h"
+
+static void gtrace(const char *what, int v);
 
 /* ---- one rank's execution of its plan ---------------------------------- */
 
@@ -319,6 +323,7 @@ static int run_device_pipe(mvx_comm_t *c, const job_t *J, hipStream_t st)
         /* slice t-2's combine is done before its blocks leave and before
          * slice t reuses its staging region */
         if (dist && hipStreamWaitEvent(st, c->pev[2 + (int)(t & 1)], 0) != hipSuccess) return MPI_ERR_OTHER;
+        if (mvxi_capturing) gtrace("pipe step", (int)t);
         for (r = 0; r < J->nr; r++) {
             mvx_xport *x = &J->t[r];
             if ((rc = x->start(x))) return rc;
@@ -326,13 +331,16 @@ static int run_device_pipe(mvx_comm_t *c, const job_t *J, hipStream_t st)
             if (dist && (rc = exec_phase_c(&X[old][r], x, st))) return rc;
             if ((rc = x->end(x))) return rc;
         }
+        if (mvxi_capturing) gtrace("pipe transfers issued", (int)t);
         if (J->t[0].lb && (rc = mvxi_lb_flush(J->t[0].lb, st))) return rc;
         if (!a) continue;
         if (hipEventRecord(c->pev[t & 1], st) != hipSuccess ||
             hipStreamWaitEvent(c->cstream, c->pev[t & 1], 0) != hipSuccess)
             return MPI_ERR_OTHER;
+        if (mvxi_capturing) gtrace("pipe combine fork", (int)t);
         for (q = 0; q < J->nr; q++)
             if ((rc = exec_phase_b(&X[cur][q], c->cstream))) return rc;
+        if (mvxi_capturing) gtrace("pipe combine issued", (int)t);
         if (hipEventRecord(c->pev[2 + (int)(t & 1)], c->cstream) != hipSuccess) return MPI_ERR_OTHER;
     }
     if ((rc = mvxi_tev(c, 3, st))) return rc;
@@ -452,10 +460,29 @@ void mvxi_graphs_clear(mvx_comm_t *c)
     for (i = 0; i < GRAPH_CACHE; i++) graph_drop(&c->w->graphs[i]);
 }
 
+/* HIP runtimes before 7.2 crash (SIGSEGV in hipGraphLaunch) on a captured
+ * graph whose work forks to a second stream and joins back -- the PIPE
+ * variant's combine stream -- while the same library on the image's 7.2
+ * runtime replays it bit-exact and single-stream captures (P2P, COLL) replay
+ * on both (tools/graph_app.c vs tests/test_gpu_multiproc.py, round 4;
+ * torch's wheel bundles a 7.0 runtime).  So PIPE is captured only on 7.2
+ * and later, and runs eagerly otherwise. */
+static int forked_capture_ok(void)
+{
+    static int ok = -1;
+    if (ok < 0) {
+        int v = 0;
+        ok = hipRuntimeGetVersion(&v) == hipSuccess && v >= 70200000;
+        (void)hipGetLastError();
+    }
+    return ok;
+}
+
 static int graph_eligible(const mvx_comm_t *c, const job_t *J)
 {
     return c->graphs && !c->graph_error && J->nr == 1 && !c->local && !c->has_ops && c->nccl && !c->timing &&
-           J->P[0].opkind == MVX_OPKIND_PREDEFINED && !J->P[0].packed;
+           J->P[0].opkind == MVX_OPKIND_PREDEFINED && !J->P[0].packed &&
+           (c->exch != MVX_EXCH_PIPE || forked_capture_ok());
 }
 
 static int graph_streams(mvx_comm_t *c)
@@ -478,6 +505,17 @@ static int graph_launch(mvx_comm_t *c, hipGraphExec_t x, hipStream_t st)
     return MPI_SUCCESS;
 }
 
+/* MVX_GRAPH_TRACE=1: each capture step on stderr (diagnostics) */
+static void gtrace(const char *what, int v)
+{
+    static int on = -1;
+    if (on < 0) {
+        const char *e = getenv("MVX_GRAPH_TRACE");
+        on = e && atoi(e) == 1;
+    }
+    if (on) fprintf(stderr, "mvx graph: %s %d\n", what, v);
+}
+
 /* capture the job on `cs` into an executable graph (nothing runs) */
 static int graph_capture(mvx_comm_t *c, const job_t *J, hipStream_t cs, hipGraphExec_t *out)
 {
@@ -485,6 +523,7 @@ static int graph_capture(mvx_comm_t *c, const job_t *J, hipStream_t cs, hipGraph
     hipError_t e;
     int rc;
     *out = NULL;
+    gtrace("begin capture, variant", c->exch);
     if (hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal) != hipSuccess) {
         (void)hipGetLastError();
         return MPI_ERR_OTHER;
@@ -492,13 +531,16 @@ static int graph_capture(mvx_comm_t *c, const job_t *J, hipStream_t cs, hipGraph
     mvxi_capturing = 1;
     rc = run_device_eager(c, J, cs);
     mvxi_capturing = 0;
+    gtrace("captured job, rc", rc);
     e = hipStreamEndCapture(cs, &g);
+    gtrace("end capture, hip error", (int)e);
     if (rc || e != hipSuccess || !g) {
         if (g) hipGraphDestroy(g);
         (void)hipGetLastError();
         return rc ? rc : MPI_ERR_OTHER;
     }
     e = hipGraphInstantiate(out, g, NULL, NULL, 0);
+    gtrace("instantiate, hip error", (int)e);
     hipGraphDestroy(g);
     if (e != hipSuccess) {
         (void)hipGetLastError();
@@ -553,7 +595,9 @@ static int run_device_graph(mvx_comm_t *c, const job_t *J, hipStream_t st)
     g->ran_exch = c->ran_exch;
     g->stamp = ++w->graph_clock;
     c->last_graph = 2;
-    return graph_launch(c, x, st);
+    rc = graph_launch(c, x, st);
+    gtrace("first launch, rc", rc);
+    return rc;
 }
 
 int mvxi_run_device(mvx_comm_t *c, const job_t *J, hipStream_t st)

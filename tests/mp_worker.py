@@ -153,6 +153,10 @@ def main():
         # fork / join onto the communicator's stream) and the stream-ordered
         # one on a torch stream; every result checked against the oracle
         report["graph_states"] = {}
+        import ctypes
+        v = ctypes.c_int()
+        ctypes.CDLL("libamdhip64.so.7").hipRuntimeGetVersion(ctypes.byref(v))
+        report["hip_runtime"] = v.value          # the runtime this process runs on (torch's)
         side = torch.cuda.Stream()
         comm.set_graphs(True)
         for name, mode, sl in modes:

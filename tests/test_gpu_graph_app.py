@@ -1,0 +1,32 @@
+"""GPU: HIP graphs of the executor from a C application (tools/graph_app.c)
+on the image's own ROCm runtime -- two processes sharing the GPU as an RCCL
+communicator (socket transport), graphs on, each exchange variant's
+Allreduce run eagerly, captured, then replayed, blocking and
+stream-ordered, every result checked in the app.  The PIPE variant's
+capture (work forked to the combine stream and joined back) replays here;
+torch's bundled 7.0 runtime crashes on it, so Python processes run PIPE
+eagerly (csrc/mvx_exec.c forked_capture_ok)."""
+import os
+import re
+import subprocess
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+APP = os.path.join(ROOT, "tools", "graph_app")
+
+
+def test_graphs_of_every_variant_from_c():
+    if not os.path.exists(APP):
+        pytest.skip("tools/graph_app not built (__graft_entry__.build)")
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    p = subprocess.run([APP], env=env, capture_output=True, text=True, timeout=150)
+    assert p.returncode == 0 and "graph_app: ok" in p.stdout, (p.returncode, p.stderr[-3000:])
+    # per rank, variant and way of calling: eager, captured, replayed
+    states = re.findall(r"rank (\d): +ok, graph state (\d) error (\d)", p.stderr)
+    assert len(states) == 36, p.stderr[-2000:]
+    for r in "01":
+        seq = [int(s) for rank, s, e in states if rank == r]
+        assert seq == [0, 2, 1] * 6, (r, seq)
+        assert all(e == "0" for rank, s, e in states)

@@ -42,6 +42,18 @@ static int exchange(ncclComm_t comm, int rank, const int *send, int *recv, hipSt
     return ncclGroupEnd() != ncclSuccess;
 }
 
+/* two sends and two receives with the same peer in one group, as PIPE's
+ * step t carries slice t's exchange and slice t - 2's distribution */
+static int exchange2(ncclComm_t comm, int rank, const int *send, int *recv, hipStream_t st)
+{
+    if (ncclGroupStart() != ncclSuccess) return 1;
+    if (ncclSend(send, N / 2, ncclInt32, 1 - rank, comm, st) != ncclSuccess) return 1;
+    if (ncclRecv(recv, N / 2, ncclInt32, 1 - rank, comm, st) != ncclSuccess) return 1;
+    if (ncclSend(send + N / 2, N / 2, ncclInt32, 1 - rank, comm, st) != ncclSuccess) return 1;
+    if (ncclRecv(recv + N / 2, N / 2, ncclInt32, 1 - rank, comm, st) != ncclSuccess) return 1;
+    return ncclGroupEnd() != ncclSuccess;
+}
+
 static int check(int rank, int *recv, int *host, int tag)
 {
     int i;
@@ -87,9 +99,76 @@ static int run(int rank, ncclUniqueId id)
         CHK(hipStreamSynchronize(st) == hipSuccess, "launch sync");
         CHK(check(rank, recv, host, i) == 0, "replayed result");
     }
-    step(rank, "ok");
     hipGraphExecDestroy(x);
     hipGraphDestroy(g);
+    /* fork / join across two streams inside the capture, as the PIPE
+     * variant does: (a) without RCCL, (b) with RCCL groups on the capturing
+     * stream and work on the joined stream between them */
+    {
+        hipStream_t s2;
+        hipEvent_t ev[4];
+        int mode;
+        CHK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking) == hipSuccess, "stream 2");
+        for (i = 0; i < 4; i++) CHK(hipEventCreateWithFlags(&ev[i], hipEventDisableTiming) == hipSuccess, "event");
+        for (mode = 0; mode < 6; mode++) {
+            int t;
+            static const char *name[] = {"fork-join capture, no RCCL", "fork-join capture with RCCL",
+                                         "pipe-shaped capture, events reused", "pipe-shaped capture, fresh events",
+                                         "two transfers per peer per group, one stream",
+                                         "pipe-shaped, two transfers per peer per group"};
+            step(rank, name[mode]);
+            CHK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal) == hipSuccess, "begin capture 2");
+            if (mode < 2) {
+                if (mode) CHK(exchange(comm, rank, send, recv, st) == 0, "captured exchange 2a");
+                else CHK(hipMemsetAsync(recv, 1, N * sizeof(int), st) == hipSuccess, "memset a");
+                CHK(hipEventRecord(ev[0], st) == hipSuccess, "record fork");
+                CHK(hipStreamWaitEvent(s2, ev[0], 0) == hipSuccess, "wait fork");
+                CHK(hipMemsetAsync(send + N / 2, 0, 4, s2) == hipSuccess, "memset on joined stream");
+                CHK(hipEventRecord(ev[1], s2) == hipSuccess, "record join");
+                if (mode) CHK(exchange(comm, rank, send, recv, st) == 0, "captured exchange 2b");
+                CHK(hipStreamWaitEvent(st, ev[1], 0) == hipSuccess, "wait join");
+            } else if (mode == 4) {
+                CHK(exchange2(comm, rank, send, recv, st) == 0, "captured double exchange");
+                CHK(exchange2(comm, rank, send, recv, st) == 0, "captured double exchange");
+            } else {
+                /* PIPE's shape: step t exchanges, waits for the work of step
+                 * t - 2 on s2, forks step t's work to s2; events of steps t
+                 * and t - 2 share a slot (mode 2) or not (mode 3) */
+                hipEvent_t fe[8], je[8];
+                for (t = 0; t < 8; t++) {
+                    if (mode != 3) { fe[t] = ev[t & 1]; je[t] = ev[2 + (t & 1)]; }
+                    else {
+                        CHK(hipEventCreateWithFlags(&fe[t], hipEventDisableTiming) == hipSuccess, "event");
+                        CHK(hipEventCreateWithFlags(&je[t], hipEventDisableTiming) == hipSuccess, "event");
+                    }
+                }
+                for (t = 0; t < 6; t++) {
+                    if (t >= 2) CHK(hipStreamWaitEvent(st, je[t - 2], 0) == hipSuccess, "wait join");
+                    if (mode == 5 && t >= 2 && t < 4)
+                        CHK(exchange2(comm, rank, send, recv, st) == 0, "captured double exchange");
+                    else
+                        CHK(exchange(comm, rank, send, recv, st) == 0, "captured exchange");
+                    if (t < 4) {
+                        CHK(hipEventRecord(fe[t], st) == hipSuccess, "record fork");
+                        CHK(hipStreamWaitEvent(s2, fe[t], 0) == hipSuccess, "wait fork");
+                        CHK(hipMemsetAsync(send + N / 2, 0, 4, s2) == hipSuccess, "memset on joined stream");
+                        CHK(hipEventRecord(je[t], s2) == hipSuccess, "record join");
+                    }
+                }
+            }
+            CHK(hipStreamEndCapture(st, &g) == hipSuccess, "end capture 2");
+            step(rank, "instantiate 2");
+            CHK(hipGraphInstantiate(&x, g, NULL, NULL, 0) == hipSuccess, "instantiate 2");
+            for (i = 0; i < 3; i++) {
+                step(rank, "launch 2");
+                CHK(hipGraphLaunch(x, st) == hipSuccess, "launch 2");
+                CHK(hipStreamSynchronize(st) == hipSuccess, "launch 2 sync");
+            }
+            hipGraphExecDestroy(x);
+            hipGraphDestroy(g);
+        }
+    }
+    step(rank, "ok");
     ncclCommDestroy(comm);
     return 0;
 }
