@@ -471,9 +471,11 @@ static int forked_capture_ok(void)
 {
     static int ok = -1;
     if (ok < 0) {
+        const char *e = getenv("MVX_GRAPH_FORK");     /* 1 / 0: force (diagnostics) */
         int v = 0;
         ok = hipRuntimeGetVersion(&v) == hipSuccess && v >= 70200000;
         (void)hipGetLastError();
+        if (e) ok = atoi(e) == 1;
     }
     return ok;
 }

@@ -159,7 +159,10 @@ def main():
         report["hip_runtime"] = v.value          # the runtime this process runs on (torch's)
         side = torch.cuda.Stream()
         comm.set_graphs(True)
+        only = os.environ.get("MVX_MP_MODES")       # e.g. "pipe": one variant only (diagnostics)
         for name, mode, sl in modes:
+            if only and name not in only.split(","):
+                continue
             assert comm.set_exchange(mode, sl) == 0
             for op, dtype in [(102, 10), (111, 17), (105, 8), (103, 6)]:
                 for coll_kind, n in (("ar", 70001), ("ar", 4096 * world * 4), ("ar", 300000), ("rs", 140000),
