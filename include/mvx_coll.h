@@ -115,7 +115,9 @@ int mvx_comm_last_exchange(MPI_Comm comm, int *mode);
  * especially).  The first call of a job runs eagerly, the second captures
  * and launches, later ones replay.  Same bits as the eager calls.  A failed
  * capture turns graphs off on the communicator (mvx_comm_last_graph reports
- * the error); mvx_comm_set_graphs(comm, 0) drops every graph. */
+ * the error).  Captured graphs live until mvx_comm_free (at most 32 per
+ * communicator; jobs past that run eagerly); mvx_comm_set_graphs(comm, 0)
+ * stops their use without destroying them. */
 int mvx_comm_set_graphs(MPI_Comm comm, int on);
 /* The last call: *state 0 eager, 1 replayed, 2 captured and launched;
  * *error the failed capture's code that turned graphs off (0: none). */

@@ -481,7 +481,8 @@ int mvx_comm_set_graphs(MPI_Comm comm, int on)
 {
     mvx_comm_t *c = mvxi_get_comm(comm);
     if (!c) return ERR_COMM_NULL_CODE;
-    if (!on) mvxi_graphs_clear(c);
+    /* turning graphs off keeps what was captured (destroyed with the
+     * communicator, mvx_exec.c); on again, they replay */
     c->graphs = on ? 1 : 0;
     c->graph_error = 0;
     return MPI_SUCCESS;

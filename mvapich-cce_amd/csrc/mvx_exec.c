@@ -427,6 +427,11 @@ static int run_device_eager(mvx_comm_t *c, const job_t *J, hipStream_t st)
  * the call runs eagerly.  Null-stream calls capture and replay on the
  * communicator's own stream, forked from and joined back to the null
  * stream with events. */
+#define G_FREE 0
+#define G_SEEN 1
+#define G_LIVE 2
+#define G_RETIRED 3
+
 static unsigned long long graph_hash(const mvx_comm_t *c, const job_t *J, hipStream_t st)
 {
     const unsigned char *b = (const unsigned char *)&J->P[0];
@@ -442,14 +447,27 @@ static unsigned long long graph_hash(const mvx_comm_t *c, const job_t *J, hipStr
 static int graph_match(const graph_ent_t *g, const mvx_comm_t *c, const job_t *J, hipStream_t st,
                        unsigned long long h)
 {
-    return g->state && g->hash == h && g->send == J->send[0] && g->recv == J->recv[0] && g->st == st &&
+    return (g->state == G_SEEN || g->state == G_LIVE) && g->hash == h && g->send == J->send[0] && g->recv == J->recv[0] && g->st == st &&
            g->pool == c->pool && g->exch == c->exch && g->slices == c->exch_slices && g->keep == c->keep &&
            !memcmp(&g->plan, &J->P[0], sizeof(mvx_plan));
 }
 
-static void graph_drop(graph_ent_t *g)
+/* Captured graphs live as long as their communicator.  Destroying one
+ * mid-life -- an LRU eviction, or a graph made on a pool since reallocated
+ * -- and then capturing another made the new graph die in hipGraphLaunch
+ * (SIGSEGV, round 4, at p = 2 and 4 over RCCL's socket transport, with an
+ * eager call between the two or not).  So nothing captured is destroyed
+ * before mvx_comm_free (mvxi_graphs_clear, run before ncclCommDestroy): a
+ * graph whose pool was reallocated is retired (state 3, never matched
+ * again), seen-once entries are the only ones replaced, and a communicator
+ * that has captured GRAPH_CACHE graphs runs its new jobs eagerly. */
+
+static void graph_destroy(graph_ent_t *g)
 {
-    if (g->state == 2 && g->exec) hipGraphExecDestroy(g->exec);
+    if ((g->state == G_LIVE || g->state == G_RETIRED) && g->exec) {
+        gtrace("destroy graph of variant", g->exch);
+        hipGraphExecDestroy(g->exec);
+    }
     memset(g, 0, sizeof *g);
 }
 
@@ -457,25 +475,17 @@ void mvxi_graphs_clear(mvx_comm_t *c)
 {
     int i;
     if (!c->w) return;
-    for (i = 0; i < GRAPH_CACHE; i++) graph_drop(&c->w->graphs[i]);
+    for (i = 0; i < GRAPH_CACHE; i++) graph_destroy(&c->w->graphs[i]);
 }
 
-/* HIP runtimes before 7.2 crash (SIGSEGV in hipGraphLaunch) on a captured
- * graph whose work forks to a second stream and joins back -- the PIPE
- * variant's combine stream -- while the same library on the image's 7.2
- * runtime replays it bit-exact and single-stream captures (P2P, COLL) replay
- * on both (tools/graph_app.c vs tests/test_gpu_multiproc.py, round 4;
- * torch's wheel bundles a 7.0 runtime).  So PIPE is captured only on 7.2
- * and later, and runs eagerly otherwise. */
+/* MVX_GRAPH_FORK=0: PIPE (whose capture forks to the combine stream and
+ * joins back) runs eagerly even with graphs on (diagnostics) */
 static int forked_capture_ok(void)
 {
     static int ok = -1;
     if (ok < 0) {
-        const char *e = getenv("MVX_GRAPH_FORK");     /* 1 / 0: force (diagnostics) */
-        int v = 0;
-        ok = hipRuntimeGetVersion(&v) == hipSuccess && v >= 70200000;
-        (void)hipGetLastError();
-        if (e) ok = atoi(e) == 1;
+        const char *e = getenv("MVX_GRAPH_FORK");
+        ok = !e || atoi(e) != 0;
     }
     return ok;
 }
@@ -556,17 +566,20 @@ static int run_device_graph(mvx_comm_t *c, const job_t *J, hipStream_t st)
 {
     mvx_work *w = mvxi_work(c);
     const unsigned long long h = graph_hash(c, J, st);
-    graph_ent_t *g = NULL, *lru = NULL;
+    graph_ent_t *g = NULL, *slot = NULL;
     hipGraphExec_t x;
     int i, rc;
     if (!w || (!st && graph_streams(c))) return run_device_eager(c, J, st);
     for (i = 0; i < GRAPH_CACHE; i++) {
         graph_ent_t *e = &w->graphs[i];
         if (graph_match(e, c, J, st, h)) { g = e; break; }
-        if (e->state && e->pool != c->pool) graph_drop(e);     /* captured on a pool since reallocated */
-        if (!lru || !e->state || (lru->state && e->stamp < lru->stamp)) lru = e;
+        if (e->state == G_LIVE && e->pool != c->pool) e->state = G_RETIRED;   /* made on a freed pool */
+        if (e->state == G_SEEN && e->pool != c->pool) e->state = G_FREE;
+        /* a slot for a new job: a free one, else the least recently seen-once */
+        if (e->state == G_FREE && (!slot || slot->state != G_FREE)) slot = e;
+        else if (e->state == G_SEEN && (!slot || (slot->state == G_SEEN && e->stamp < slot->stamp))) slot = e;
     }
-    if (g && g->state == 2) {                                  /* replay */
+    if (g && g->state == G_LIVE) {                             /* replay */
         g->stamp = ++w->graph_clock;
         c->ran_exch = g->ran_exch;
         c->last_graph = 1;
@@ -575,25 +588,25 @@ static int run_device_graph(mvx_comm_t *c, const job_t *J, hipStream_t st)
     if (!g) {                                                  /* first sighting: eager */
         c->last_graph = 0;
         rc = run_device_eager(c, J, st);
-        if (rc) return rc;
-        graph_drop(lru);
-        lru->state = 1;
-        lru->hash = graph_hash(c, J, st);                      /* the pool as the call left it */
-        lru->plan = J->P[0];
-        lru->send = J->send[0]; lru->recv = J->recv[0]; lru->st = st; lru->pool = c->pool;
-        lru->exch = c->exch; lru->slices = c->exch_slices; lru->keep = c->keep;
-        lru->stamp = ++w->graph_clock;
+        if (rc || !slot) return rc;                            /* no slot: every one holds a graph */
+        memset(slot, 0, sizeof *slot);
+        slot->state = G_SEEN;
+        slot->hash = graph_hash(c, J, st);                     /* the pool as the call left it */
+        slot->plan = J->P[0];
+        slot->send = J->send[0]; slot->recv = J->recv[0]; slot->st = st; slot->pool = c->pool;
+        slot->exch = c->exch; slot->slices = c->exch_slices; slot->keep = c->keep;
+        slot->stamp = ++w->graph_clock;
         return MPI_SUCCESS;
     }
     rc = graph_capture(c, J, st ? st : c->gstream, &x);       /* second sighting: capture */
     if (rc) {
         c->graph_error = rc;
-        graph_drop(g);
+        memset(g, 0, sizeof *g);
         c->last_graph = 0;
         return run_device_eager(c, J, st);
     }
     g->exec = x;
-    g->state = 2;
+    g->state = G_LIVE;
     g->ran_exch = c->ran_exch;
     g->stamp = ++w->graph_clock;
     c->last_graph = 2;

@@ -170,9 +170,9 @@ MVXI void mvxi_stage_release(stage_res_t *S);
  * one hipGraphLaunch instead of the host issue of every group and kernel.
  * The key is everything the captured work depends on: the plan, the
  * buffers, the stream, the staging pool and the variant. */
-#define GRAPH_CACHE 16
+#define GRAPH_CACHE 32
 typedef struct {
-    int state;                  /* 0 free, 1 seen once (ran eagerly), 2 captured */
+    int state;                  /* 0 free, 1 seen once (ran eagerly), 2 captured, 3 retired (mvx_exec.c) */
     unsigned long long hash;
     mvx_plan plan;
     const char *send;
