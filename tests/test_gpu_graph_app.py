@@ -2,10 +2,9 @@
 on the image's own ROCm runtime -- two processes sharing the GPU as an RCCL
 communicator (socket transport), graphs on, each exchange variant's
 Allreduce run eagerly, captured, then replayed, blocking and
-stream-ordered, every result checked in the app.  The PIPE variant's
-capture (work forked to the combine stream and joined back) replays here;
-torch's bundled 7.0 runtime crashes on it, so Python processes run PIPE
-eagerly (csrc/mvx_exec.c forked_capture_ok)."""
+stream-ordered, every result checked in the app.
+The same library from Python runs on torch's bundled HIP / RCCL instead
+(tests/test_gpu_multiproc.py::test_graphs_rccl_net)."""
 import os
 import re
 import subprocess
