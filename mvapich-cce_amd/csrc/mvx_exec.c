@@ -255,11 +255,24 @@ int mvxi_job_layout(mvx_comm_t *c, rank_exec_t *X, const job_t *J, const mvx_pla
 }
 
 /* ---- exchange variants (MVX_EXCH_*) -------------------------------------
- * PIPE: the plan runs in slices; slice t's exchange and slice t-2's
- * distribution go in one transfer group while slice t-1 is combined on a
- * second stream, so xGMI and HBM work at once.  Slices keep every block
- * boundary (plan_slice), so the bits are the unsliced plan's.  The slice
- * plans and per-slice rank tables are the communicator's (mvx_work). */
+ * PIPE: phase A runs in slices, one transfer group per slice on the call's
+ * stream; slice t's combine runs on a second stream as soon as slice t has
+ * arrived, while slice t + 1 is still on the links; phase C is one transfer
+ * group after the last combine, as P2P's.  On links that bound the step, the
+ * combine is then exposed for one slice instead of whole.  Slices keep every
+ * block boundary (plan_slice), so the bits are the unsliced plan's.
+ *
+ * Host cost (round 4, tools/graph_cost.c): every cross-stream dependency
+ * (an event record or wait) costs about 4-5 us to issue on this runtime, a
+ * replayed graph included, and every send / receive about 0.7-1 us.  So
+ * the schedule uses one fork per slice and a single join (2 S + 2 event
+ * operations, S + 1 transfer groups, 2(p - 1) operations per slice of A and
+ * one phase C) -- not a join per slice and a group per step carrying slice
+ * t's exchange with slice t - 2's distribution, which cost 4 S event
+ * operations and twice the transfers for the same overlap where the links
+ * are the bound.  Every slice has its own staging region (together about
+ * the unsliced plan's).  The slice plans and rank tables are the
+ * communicator's (mvx_work). */
 
 static int pipe_streams(mvx_comm_t *c)
 {
@@ -283,6 +296,16 @@ static int run_device_plain(mvx_comm_t *c, const job_t *J, hipStream_t st)
     return mvxi_exec_group(X, J->t, J->nr, st, c);
 }
 
+/* rank r's tables for slice t (staging region t) */
+static void pipe_slice(mvx_comm_t *c, const job_t *J, int r, long t, long cs, size_t region, const size_t *off,
+                       rank_exec_t *X0, rank_exec_t *X, mvx_plan *Q)
+{
+    *X = X0[r];
+    mvxi_plan_slice(&J->P[r], t, cs, Q);
+    X->P = Q;
+    X->pool = c->pool + (size_t)t * region + off[r];
+}
+
 static int run_device_pipe(mvx_comm_t *c, const job_t *J, hipStream_t st)
 {
     mvx_work *w = mvxi_work(c);
@@ -290,12 +313,14 @@ static int run_device_pipe(mvx_comm_t *c, const job_t *J, hipStream_t st)
     mvx_plan (*pl)[MVX_MAXP];
     size_t off[MVX_MAXP], region;
     long span = 0, cs, nsl, t;
-    int r, rc, q;
+    int r, rc, tmp = 0;
     const int ns = c->exch_slices > 0 ? c->exch_slices : 4;
     if (!w) return MPI_ERR_INTERN;
     X0 = w->px0; X = w->px; pl = w->pipe;
-    for (r = 0; r < J->nr; r++)
+    for (r = 0; r < J->nr; r++) {
         if (mvxi_plan_span(&J->P[r]) > span) span = mvxi_plan_span(&J->P[r]);
+        tmp |= J->P[r].c_dst_tmp;
+    }
     cs = (span + ns - 1) / ns;
     cs = (cs + 255) & ~255L;
     nsl = (span + cs - 1) / cs;
@@ -308,41 +333,43 @@ static int run_device_pipe(mvx_comm_t *c, const job_t *J, hipStream_t st)
         X0[r].recvbuf = J->recv[r];
     }
     region = mvxi_region_layout(c, X0, J, pl[0], off);   /* slice 0 is the largest */
-    if ((rc = mvxi_grow(&c->pool, &c->pool_bytes, 2 * region))) return rc;
+    if ((rc = mvxi_grow(&c->pool, &c->pool_bytes, (size_t)nsl * region))) return rc;
     if ((rc = mvxi_tev(c, 0, st))) return rc;
-    for (t = 0; t < nsl + 2; t++) {
-        const int a = t < nsl, dist = t >= 2;
-        const int cur = (int)(t % 3), old = (int)((t + 1) % 3);   /* old = (t - 2) % 3 */
-        if (a)
-            for (r = 0; r < J->nr; r++) {
-                X[cur][r] = X0[r];
-                mvxi_plan_slice(&J->P[r], t, cs, &pl[cur][r]);
-                X[cur][r].P = &pl[cur][r];
-                X[cur][r].pool = c->pool + (t & 1) * region + off[r];
-            }
-        /* slice t-2's combine is done before its blocks leave and before
-         * slice t reuses its staging region */
-        if (dist && hipStreamWaitEvent(st, c->pev[2 + (int)(t & 1)], 0) != hipSuccess) return MPI_ERR_OTHER;
-        if (mvxi_capturing) gtrace("pipe step", (int)t);
+    for (t = 0; t < nsl; t++) {
+        const int k = (int)(t & 1);
+        if (mvxi_capturing) gtrace("pipe slice", (int)t);
         for (r = 0; r < J->nr; r++) {
-            mvx_xport *x = &J->t[r];
-            if ((rc = x->start(x))) return rc;
-            if (a && (rc = exec_phase_a(&X[cur][r], x, st))) return rc;
-            if (dist && (rc = exec_phase_c(&X[old][r], x, st))) return rc;
-            if ((rc = x->end(x))) return rc;
+            pipe_slice(c, J, r, t, cs, region, off, X0, &X[k][r], &pl[k][r]);
+            if ((rc = exec_phase_a(&X[k][r], &J->t[r], st))) return rc;
         }
-        if (mvxi_capturing) gtrace("pipe transfers issued", (int)t);
         if (J->t[0].lb && (rc = mvxi_lb_flush(J->t[0].lb, st))) return rc;
-        if (!a) continue;
-        if (hipEventRecord(c->pev[t & 1], st) != hipSuccess ||
-            hipStreamWaitEvent(c->cstream, c->pev[t & 1], 0) != hipSuccess)
+        if (hipEventRecord(c->pev[k], st) != hipSuccess || hipStreamWaitEvent(c->cstream, c->pev[k], 0) != hipSuccess)
             return MPI_ERR_OTHER;
-        if (mvxi_capturing) gtrace("pipe combine fork", (int)t);
-        for (q = 0; q < J->nr; q++)
-            if ((rc = exec_phase_b(&X[cur][q], c->cstream))) return rc;
-        if (mvxi_capturing) gtrace("pipe combine issued", (int)t);
-        if (hipEventRecord(c->pev[2 + (int)(t & 1)], c->cstream) != hipSuccess) return MPI_ERR_OTHER;
+        for (r = 0; r < J->nr; r++)
+            if ((rc = exec_phase_b(&X[k][r], c->cstream))) return rc;
     }
+    if (hipEventRecord(c->pev[2], c->cstream) != hipSuccess || hipStreamWaitEvent(st, c->pev[2], 0) != hipSuccess)
+        return MPI_ERR_OTHER;
+    if (mvxi_capturing) gtrace("pipe combines joined", (int)nsl);
+    /* phase C: the unsliced plan's when the combined blocks are in recvbuf;
+     * a non-root Reduce's temporary results are per slice, in one group */
+    for (r = 0; r < J->nr; r++) {
+        mvx_xport *x = &J->t[r];
+        if (!tmp) {
+            X[0][r] = X0[r];
+            X[0][r].P = &J->P[r];
+            if ((rc = exec_phase_c(&X[0][r], x, st))) return rc;
+            continue;
+        }
+        if ((rc = x->start(x))) return rc;
+        for (t = 0; t < nsl && !rc; t++) {
+            pipe_slice(c, J, r, t, cs, region, off, X0, &X[0][r], &pl[0][r]);
+            rc = exec_phase_c(&X[0][r], x, st);
+        }
+        if (rc) { x->end(x); return rc; }
+        if ((rc = x->end(x))) return rc;
+    }
+    if (J->t[0].lb && (rc = mvxi_lb_flush(J->t[0].lb, st))) return rc;
     if ((rc = mvxi_tev(c, 3, st))) return rc;
     if (c->timing) c->tev_kind = TEV_TOTAL;
     return MPI_SUCCESS;

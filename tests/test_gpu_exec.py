@@ -196,10 +196,11 @@ def test_argument_test_order(mvx):
 @pytest.mark.parametrize("slices", [2, 3, 5])
 @pytest.mark.parametrize("p", [2, 3, 4, 8, 9])
 def test_pipelined_exchange_matches_reference(mvx, oracle, slices, p):
-    """MVX_EXCH_PIPE: slice t's exchange + slice t-2's distribution in one
-    transfer group while slice t-1 combines on a second stream (loopback
-    transport here, the RCCL executor's phase code) -- same bits as the
-    reference schedule for every collective, role-sensitive ops included."""
+    """MVX_EXCH_PIPE: slice t's exchange while slice t-1 combines on a
+    second stream, then one distribution group (per-slice groups for a
+    non-root Reduce's temporary results); loopback transport here, the RCCL
+    executor's phase code -- same bits as the reference schedule for every
+    collective, role-sensitive ops included."""
     import torch
     comm = mvx.Comm.local_ranks(p, 0)
     assert comm.set_exchange(mvx.EXCH_PIPE, slices) == 0
