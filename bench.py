@@ -46,9 +46,17 @@ CONFIGS = {
 # exchange variants: (mvx_comm_set_exchange mode, slices, mvx_comm_set_graphs).
 # The "+g" ones capture each call into a HIP graph once and replay it (one
 # hipGraphLaunch per step in place of the host issue of every RCCL group and
-# kernel); tried last, after every eager variant has had its turn.
+# kernel); tried last, after every eager variant has had its turn, and only
+# with --graphs: they have run over RCCL's socket transport on one GPU, never
+# over xGMI, and a fault there would take the whole line with it (DESIGN.md
+# section 6).
 EXCH = {"p2p": (0, 0, 0), "pipe": (1, 4, 0), "pipe2": (1, 2, 0), "pipe8": (1, 8, 0), "coll": (2, 0, 0),
         "p2p+g": (0, 0, 1), "pipe+g": (1, 4, 1), "pipe2+g": (1, 2, 1), "pipe8+g": (1, 8, 1), "coll+g": (2, 0, 1)}
+
+
+def auto_variants(args):
+    """--exchange auto: the eager variants, then the graph ones if --graphs"""
+    return [k for k, v in EXCH.items() if args.graphs or not v[2]]
 
 
 def apply_variant(comm, name):
@@ -84,8 +92,10 @@ def parse(argv=None):
                     help="input sets used round-robin (4 x 512 MiB keeps every step out of the 256 MiB "
                          "Infinity Cache: the number is HBM-bound, not cache-bound)")
     ap.add_argument("--exchange", default="auto",
-                    help="auto: every variant (EXCH), the fastest clean one makes the line; or a comma list "
-                         "of them")
+                    help="auto: every eager variant of EXCH (and the graph ones with --graphs), the "
+                         "fastest clean one makes the line; or a comma list of them")
+    ap.add_argument("--graphs", action="store_true",
+                    help="auto also tries the HIP-graph variants (the '+g' ones of EXCH)")
     ap.add_argument("--tune-steps", type=int, default=5)
     ap.add_argument("--extra-configs", default="auto",
                     help="N > 1: more BASELINE configs measured after the line, on the same communicator "
@@ -1065,7 +1075,7 @@ def run_multi(args, mvx, dev, world, rank, local, clock):
     # measured again only if its tuning steps ran faster -- so a line exists
     # before any riskier variant runs, and a variant that wedges the GPU for
     # good ends the run with the line already measured rather than with none.
-    names = list(EXCH) if args.exchange == "auto" else args.exchange.split(",")
+    names = auto_variants(args) if args.exchange == "auto" else args.exchange.split(",")
     tried = {}
 
     for name in names:

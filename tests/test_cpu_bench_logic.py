@@ -119,3 +119,13 @@ def test_env_echo_keeps_only_the_knobs():
     e = bench.env_echo({"NCCL_DEBUG": "INFO", "HOME": "/root", "MVX_EXCHANGE": "coll", "RCCL_X": "1",
                         "HSA_ENABLE_IPC_MODE_LEGACY": "0"})
     assert e == {"HSA_ENABLE_IPC_MODE_LEGACY": "0", "MVX_EXCHANGE": "coll", "NCCL_DEBUG": "INFO", "RCCL_X": "1"}
+
+
+def test_auto_variants_leave_graphs_to_the_flag():
+    """--exchange auto tries the eager variants; the HIP-graph ones only with
+    --graphs (untested over xGMI), after the eager ones"""
+    eager = bench.auto_variants(bench.parse([]))
+    assert eager == ["p2p", "pipe", "pipe2", "pipe8", "coll"]
+    both = bench.auto_variants(bench.parse(["--graphs"]))
+    assert both[:5] == eager and all(n.endswith("+g") for n in both[5:]) and len(both) == 10
+    assert bench.parse(["--exchange", "pipe+g"]).exchange == "pipe+g"

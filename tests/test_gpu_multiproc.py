@@ -217,7 +217,7 @@ def test_bench_multi_gpu_leg_rccl_net(cfg):
     """bench.py's N > 1 leg on RCCL communicators (2 ranks sharing the GPU,
     RCCL's socket transport): every exchange variant -- COLL as
     ncclAllToAll + ncclAllGather -- ran as itself with parity bit-exact."""
-    p = _bench_host(cfg, transport="rccl-net")
+    p = _bench_host(cfg, transport="rccl-net", extra_args=("--graphs",))
     assert p.returncode == 0, p.stderr[-3000:]
     line = [x for x in p.stdout.splitlines() if x.startswith("{")]
     assert len(line) == 1, p.stdout[-2000:]
@@ -248,7 +248,8 @@ def test_bench_full_size_eight_ranks_rccl_net():
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"),
-           "--gpus", "8", "--steps", "2", "--warmup", "1", "--tune-steps", "1", "--transport", "rccl-net"]
+           "--gpus", "8", "--steps", "2", "--warmup", "1", "--tune-steps", "1", "--transport", "rccl-net",
+           "--graphs"]
     p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=420)
     assert p.returncode == 0, p.stderr[-3000:]
     line = [x for x in p.stdout.splitlines() if x.startswith("{")]
