@@ -271,8 +271,10 @@ int mvxi_job_layout(mvx_comm_t *c, rank_exec_t *X, const job_t *J, const mvx_pla
  * t's exchange with slice t - 2's distribution, which cost 4 S event
  * operations and twice the transfers for the same overlap where the links
  * are the bound.  Every slice has its own staging region (together about
- * the unsliced plan's).  The slice plans and rank tables are the
- * communicator's (mvx_work). */
+ * the unsliced plan's) and a non-root Reduce's temporary result is kept
+ * whole, so phase C is the unsliced plan's on every rank and the ranks'
+ * messages pair up whatever each one's own plan holds.  The slice plans
+ * and rank tables are the communicator's (mvx_work). */
 
 static int pipe_streams(mvx_comm_t *c)
 {
@@ -296,14 +298,16 @@ static int run_device_plain(mvx_comm_t *c, const job_t *J, hipStream_t st)
     return mvxi_exec_group(X, J->t, J->nr, st, c);
 }
 
-/* rank r's tables for slice t (staging region t) */
-static void pipe_slice(mvx_comm_t *c, const job_t *J, int r, long t, long cs, size_t region, const size_t *off,
-                       rank_exec_t *X0, rank_exec_t *X, mvx_plan *Q)
+/* rank r's tables for slice t (staging region t); a non-root Reduce's
+ * temporary result goes to its place in the unsliced temporary at tmp */
+static void pipe_slice(const job_t *J, int r, long t, long cs, char *region_base, char *tmp,
+                       const rank_exec_t *X0, rank_exec_t *X, mvx_plan *Q)
 {
     *X = X0[r];
     mvxi_plan_slice(&J->P[r], t, cs, Q);
     X->P = Q;
-    X->pool = c->pool + (size_t)t * region + off[r];
+    X->pool = region_base;
+    if (Q->c_dst_tmp) X->tmp_off = (size_t)(tmp + t * cs * Q->esize - region_base);
 }
 
 static int run_device_pipe(mvx_comm_t *c, const job_t *J, hipStream_t st)
@@ -311,15 +315,16 @@ static int run_device_pipe(mvx_comm_t *c, const job_t *J, hipStream_t st)
     mvx_work *w = mvxi_work(c);
     rank_exec_t *X0, (*X)[MVX_MAXP];
     mvx_plan (*pl)[MVX_MAXP];
-    size_t off[MVX_MAXP], region;
+    size_t off[MVX_MAXP], toff[MVX_MAXP], region, tmp_bytes = 0;
     long span = 0, cs, nsl, t;
-    int r, rc, tmp = 0;
+    int r, rc;
     const int ns = c->exch_slices > 0 ? c->exch_slices : 4;
     if (!w) return MPI_ERR_INTERN;
     X0 = w->px0; X = w->px; pl = w->pipe;
     for (r = 0; r < J->nr; r++) {
         if (mvxi_plan_span(&J->P[r]) > span) span = mvxi_plan_span(&J->P[r]);
-        tmp |= J->P[r].c_dst_tmp;
+        toff[r] = tmp_bytes;
+        if (J->P[r].c_dst_tmp) tmp_bytes = al256(tmp_bytes + (size_t)(J->P[r].c_cnt * J->P[r].esize));
     }
     cs = (span + ns - 1) / ns;
     cs = (cs + 255) & ~255L;
@@ -333,13 +338,14 @@ static int run_device_pipe(mvx_comm_t *c, const job_t *J, hipStream_t st)
         X0[r].recvbuf = J->recv[r];
     }
     region = mvxi_region_layout(c, X0, J, pl[0], off);   /* slice 0 is the largest */
-    if ((rc = mvxi_grow(&c->pool, &c->pool_bytes, (size_t)nsl * region))) return rc;
+    if ((rc = mvxi_grow(&c->pool, &c->pool_bytes, (size_t)nsl * region + tmp_bytes))) return rc;
     if ((rc = mvxi_tev(c, 0, st))) return rc;
     for (t = 0; t < nsl; t++) {
         const int k = (int)(t & 1);
         if (mvxi_capturing) gtrace("pipe slice", (int)t);
         for (r = 0; r < J->nr; r++) {
-            pipe_slice(c, J, r, t, cs, region, off, X0, &X[k][r], &pl[k][r]);
+            pipe_slice(J, r, t, cs, c->pool + (size_t)t * region + off[r], c->pool + (size_t)nsl * region + toff[r],
+                       X0, &X[k][r], &pl[k][r]);
             if ((rc = exec_phase_a(&X[k][r], &J->t[r], st))) return rc;
         }
         if (J->t[0].lb && (rc = mvxi_lb_flush(J->t[0].lb, st))) return rc;
@@ -351,23 +357,17 @@ static int run_device_pipe(mvx_comm_t *c, const job_t *J, hipStream_t st)
     if (hipEventRecord(c->pev[2], c->cstream) != hipSuccess || hipStreamWaitEvent(st, c->pev[2], 0) != hipSuccess)
         return MPI_ERR_OTHER;
     if (mvxi_capturing) gtrace("pipe combines joined", (int)nsl);
-    /* phase C: the unsliced plan's when the combined blocks are in recvbuf;
-     * a non-root Reduce's temporary results are per slice, in one group */
+    /* phase C unsliced, as P2P's: the combined blocks are whole in recvbuf,
+     * or in the unsliced temporary (a non-root Reduce), so every rank sends
+     * and receives the same messages whatever its own plan holds */
     for (r = 0; r < J->nr; r++) {
-        mvx_xport *x = &J->t[r];
-        if (!tmp) {
-            X[0][r] = X0[r];
-            X[0][r].P = &J->P[r];
-            if ((rc = exec_phase_c(&X[0][r], x, st))) return rc;
-            continue;
+        X[0][r] = X0[r];
+        X[0][r].P = &J->P[r];
+        if (J->P[r].c_dst_tmp) {
+            X[0][r].pool = c->pool + (size_t)nsl * region + toff[r];
+            X[0][r].tmp_off = 0;
         }
-        if ((rc = x->start(x))) return rc;
-        for (t = 0; t < nsl && !rc; t++) {
-            pipe_slice(c, J, r, t, cs, region, off, X0, &X[0][r], &pl[0][r]);
-            rc = exec_phase_c(&X[0][r], x, st);
-        }
-        if (rc) { x->end(x); return rc; }
-        if ((rc = x->end(x))) return rc;
+        if ((rc = exec_phase_c(&X[0][r], &J->t[r], st))) return rc;
     }
     if (J->t[0].lb && (rc = mvxi_lb_flush(J->t[0].lb, st))) return rc;
     if ((rc = mvxi_tev(c, 3, st))) return rc;
