@@ -132,7 +132,9 @@ def main():
         # draw, through the one-rank-per-process path)
         for i in range(int(os.environ.get("MVX_MP_CASES", "120"))):
             rng = np.random.default_rng(4242 + i)
-            name, mode, sl = modes[int(rng.integers(0, len(modes)))]
+            # MVX_MP_MODES=pipe: draw that variant only (same rng sequence)
+            pool = [m for m in modes if m[0] in os.environ.get("MVX_MP_MODES", m[0]).split(",")]
+            name, mode, sl = pool[int(rng.integers(0, len(modes))) % len(pool)]
             assert comm.set_exchange(mode, int(rng.integers(2, 6)) if mode == mvx.EXCH_PIPE else sl) == 0
             coll = str(rng.choice(["ar", "ar", "red", "rs", "scan"]))
             dtype = int(rng.choice(T.ALL_TYPES))
