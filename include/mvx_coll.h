@@ -258,13 +258,14 @@ int PMPI_Op_free(MPI_Op *);
 /* ---- stream-ordered variants (device buffers only) ---------------------
  * Calls on one communicator share its staging pool: issue them on one
  * stream (as MPI orders a communicator's collectives), or synchronise the
- * streams between calls.
+ * streams between calls -- RCCL does not order one communicator's transfers
+ * issued on two streams against each other (round 4: such a schedule did
+ * not finish at p = 8, tools/graph_cost.c).
  *
- * Buffer kinds must agree across ranks within one call: every rank passes
- * device buffers, or every rank passes host buffers.  Host-buffer calls
- * move in slices (lengths fixed by count, p and the type, the same on every
- * rank); device-buffer calls move whole blocks; a mix pairs transfers of
- * different sizes. */
+ * Buffer kinds may differ across ranks: a host buffer at p > 1 is mirrored
+ * in HBM and its blocks move as a device buffer's do.  Only the opt-in
+ * sliced host pipeline (mvx_comm_set_host_pipeline) moves host buffers in
+ * slices, and then every rank of a call must pass host buffers. */
 int mvx_reduce_async(const void *sendbuf, void *recvbuf, int count,
                      MPI_Datatype datatype, MPI_Op op, int root, MPI_Comm comm,
                      void *hip_stream);
