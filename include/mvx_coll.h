@@ -90,9 +90,9 @@ int mvx_comm_reserve(MPI_Comm comm, size_t bytes);
 /* How a communicator moves blocks between ranks (device buffers).  All
  * variants compute the same bits; they differ in how xGMI is driven.
  *   MVX_EXCH_P2P   phases as grouped ncclSend / ncclRecv (default)
- *   MVX_EXCH_PIPE  the plan in `slices` slices: the exchange of slice t and
- *                  the distribution of slice t-2 share one transfer group
- *                  while slice t-1 is combined on a second stream
+ *   MVX_EXCH_PIPE  the exchange in `slices` slices, each combined on a
+ *                  second stream as it arrives while the next is on the
+ *                  links; one distribution group after the last combine
  *   MVX_EXCH_COLL  ncclAllToAll + in-place ncclAllGather when every rank
  *                  holds p equal blocks (Allreduce / Reduce_scatter with
  *                  count % p == 0, p a power of two); P2P otherwise
