@@ -2,8 +2,8 @@
  * graph_cost.c -- where does the host time of a PIPE-shaped call go, eager
  * and as a replayed HIP graph?  p processes (forked before any HIP call)
  * share the box's one GPU as p "hosts" (NCCL_HOSTID, RCCL's socket
- * transport, as transport.rccl_net_env) and issue PIPE's shape for S slices:
- * step t groups slice t's exchange and slice t - 2's distribution (one
+ * transport, as transport.rccl_net_env) and issue round 3's PIPE shape for S
+ * slices: step t groups slice t's exchange and slice t - 2's distribution (one
  * send / receive per peer and phase), slice t's combine runs on a second
  * stream forked and joined through events (a memset stands in for it).
  * The second shape is round 4's PIPE: a fork to the combine stream per
