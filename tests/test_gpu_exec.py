@@ -288,3 +288,89 @@ def test_pageable_ragged_sizes(mvx, oracle, n, p, coll):
             T.assert_same(op, dtype, recvs[q], R0[q], typemap_only=True)
     finally:
         comm.free()
+
+
+def test_two_communicators_interleaved(mvx, oracle):
+    """Executor state is per communicator (mvx_work: staging pool, slice
+    plans, rank tables): two communicators issuing stream-ordered calls on
+    two streams, interleaved and in flight together -- a PIPE one (p = 4,
+    3 slices) and a P2P one (p = 3) -- each get the reference's bits."""
+    import torch
+    ca, cb = mvx.Comm.local_ranks(4, 0), mvx.Comm.local_ranks(3, 0)
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+    try:
+        assert ca.set_exchange(mvx.EXCH_PIPE, 3) == 0
+        jobs = []
+        for it in range(4):
+            for comm, p, st, coll, n in ((ca, 4, sa, "ar", 300001 + it), (cb, 3, sb, "rs", 90001 + it)):
+                cnts = [n // p + (r % 2) for r in range(p)] if coll == "rs" else None
+                tot = sum(cnts) if cnts else n
+                S = [T.rand_vec(10, tot, 71 * it + 7 * p + r) for r in range(p)]
+                ds = [T.to_dev(s) for s in S]
+                drs = [torch.zeros(max(cnts[q] if cnts else n, 1) * 4, dtype=torch.uint8, device="cuda")
+                       for q in range(p)]
+                torch.cuda.synchronize()          # inputs written before the other streams read them
+                r = _call_on(comm, coll, ds, drs, cnts if cnts else n, st)
+                assert r[0] == 0, r
+                jobs.append((coll, p, S, drs, cnts if cnts else n, ds))
+        torch.cuda.synchronize()
+        for coll, p, S, drs, nc, _ in jobs:
+            R0 = [np.zeros(max(nc[q] if coll == "rs" else nc, 1), np.float32) for q in range(p)]
+            rref = _oracle_coll(oracle, coll, S, R0, nc, 10, 102)
+            assert rref == [0] * p
+            for q in range(p):
+                cnt = nc[q] if coll == "rs" else nc
+                T.assert_same(102, 10, T.from_dev(drs[q])[: cnt * 4], R0[q][:cnt], typemap_only=True)
+    finally:
+        ca.free()
+        cb.free()
+
+
+def _call_on(comm, coll, sends, recvs, n_or_cnts, stream):
+    if coll == "ar":
+        return comm.allreduce_multi(sends, recvs, n_or_cnts, 10, 102, stream)
+    return comm.reduce_scatter_multi(sends, recvs, n_or_cnts, 10, 102, stream)
+
+
+def test_two_communicators_from_two_threads(mvx, oracle):
+    """Blocking calls on two communicators from two host threads at once
+    (each communicator's calls stay on one thread, as MPI orders them)."""
+    import threading
+    import torch
+    comms = [mvx.Comm.local_ranks(4, 0), mvx.Comm.local_ranks(2, 0)]
+    assert comms[0].set_exchange(mvx.EXCH_PIPE, 4) == 0
+    errors, done = [], []
+
+    def worker(w):
+        try:
+            torch.cuda.set_device(0)
+            comm, p = comms[w], (4, 2)[w]
+            for it in range(5):
+                n = 200003 + 1000 * it + w
+                S = [T.rand_vec(10, n, 1000 * w + 10 * it + r) for r in range(p)]
+                ds = [T.to_dev(s) for s in S]
+                drs = [torch.zeros(n * 4, dtype=torch.uint8, device="cuda") for _ in range(p)]
+                torch.cuda.synchronize()
+                r, rcs = _call(comm, "ar", ds, drs, n, 10, 102)
+                if r != 0:
+                    errors.append((w, it, r))
+                    return
+                R0 = [np.zeros(n, np.float32) for _ in range(p)]
+                _oracle_coll(oracle, "ar", S, R0, n, 10, 102)
+                for q in range(p):
+                    T.assert_same(102, 10, T.from_dev(drs[q])[: n * 4], R0[q], typemap_only=True)
+            done.append(w)
+        except Exception as e:            # reported below
+            errors.append((w, repr(e)[:300]))
+
+    th = [threading.Thread(target=worker, args=(w,)) for w in range(2)]
+    try:
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(120)
+        assert not any(t.is_alive() for t in th), "a worker did not finish"
+        assert not errors and sorted(done) == [0, 1], errors
+    finally:
+        for c in comms:
+            c.free()
