@@ -276,36 +276,15 @@ int mvxi_job_layout(mvx_comm_t *c, rank_exec_t *X, const job_t *J, const mvx_pla
  * messages pair up whatever each one's own plan holds.  The slice plans
  * and rank tables are the communicator's (mvx_work). */
 
-/* The combine stream needs a hardware queue of its own: HIP spreads streams
- * over GPU_MAX_HW_QUEUES queues, and two streams that share a queue run in
- * submission order, so slice t + 1's transfers waited behind slice t's
- * combine (round 4, tools/prof_pipe_overlap.sh: both streams on one queue,
- * 0.1 % of the combine time under a transfer).  MVX_PIPE_STREAM selects how
- * it is made: "priority" (default; the greatest stream priority, whose
- * streams HIP takes from a queue pool of their own), "cumask" (a stream
- * with every CU in its mask, which HIP gives a queue of its own) or "plain". */
-static hipError_t combine_stream(hipStream_t *s)
-{
-    const char *e = getenv("MVX_PIPE_STREAM");
-    int least = 0, greatest = 0;
-    if (e && !strcmp(e, "plain")) return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
-    if (e && !strcmp(e, "cumask")) {
-        uint32_t mask[16];
-        memset(mask, 0xff, sizeof mask);        /* 512 CUs: more than any part has */
-        return hipExtStreamCreateWithCUMask(s, 16, mask);
-    }
-    if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) {
-        (void)hipGetLastError();
-        return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
-    }
-    return hipStreamCreateWithPriority(s, hipStreamNonBlocking, greatest);
-}
-
+/* The combine stream needs a hardware queue of its own (mvxi_queue_stream):
+ * on a shared queue slice t + 1's transfers waited behind slice t's combine
+ * (round 4, tools/prof_pipe_overlap.sh: 0.1 % of the combine time under a
+ * transfer; 75 % of it with 4 slices on a queue of its own). */
 static int pipe_streams(mvx_comm_t *c)
 {
     int i;
     if (c->cstream) return MPI_SUCCESS;
-    if (combine_stream(&c->cstream) != hipSuccess) return MPI_ERR_OTHER;
+    if (mvxi_queue_stream(&c->cstream, "MVX_PIPE_STREAM", "priority") != hipSuccess) return MPI_ERR_OTHER;
     for (i = 0; i < 4; i++)
         if (hipEventCreateWithFlags(&c->pev[i], hipEventDisableTiming) != hipSuccess) return MPI_ERR_OTHER;
     return MPI_SUCCESS;

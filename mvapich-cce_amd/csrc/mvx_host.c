@@ -309,3 +309,27 @@ int mvxi_buf_kind_range(const void *p, size_t bytes)
     pthread_mutex_unlock(&g_reg.mu);
     return MVX_BUF_PINNED;
 }
+
+
+/* A stream for work that must run beside the caller's stream.  HIP spreads
+ * streams over GPU_MAX_HW_QUEUES hardware queues, and two streams that share
+ * a queue run in submission order whatever their events say.  Mode (env
+ * `env`, else `dflt`): "priority" -- the greatest stream priority, whose
+ * streams HIP takes from a queue pool of their own; "cumask" -- every CU in
+ * the stream's mask, which HIP gives a queue of its own; "plain". */
+hipError_t mvxi_queue_stream(hipStream_t *s, const char *env, const char *dflt)
+{
+    const char *e = getenv(env);
+    int least = 0, greatest = 0;
+    if (!e) e = dflt;
+    if (!strcmp(e, "cumask")) {
+        uint32_t mask[16];
+        memset(mask, 0xff, sizeof mask);        /* 512 CUs: more than any part has */
+        return hipExtStreamCreateWithCUMask(s, 16, mask);
+    }
+    if (strcmp(e, "priority") || hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) {
+        (void)hipGetLastError();
+        return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+    }
+    return hipStreamCreateWithPriority(s, hipStreamNonBlocking, greatest);
+}

@@ -50,8 +50,8 @@ static int hop_init(size_t slot, size_t dev)
 {
     int b;
     if (!g_hop.s[0]) {
-        if (hipStreamCreateWithFlags(&g_hop.s[0], hipStreamNonBlocking) != hipSuccess ||
-            hipStreamCreateWithFlags(&g_hop.s[1], hipStreamNonBlocking) != hipSuccess)
+        if (mvxi_queue_stream(&g_hop.s[0], "MVX_STAGE_STREAM", "plain") != hipSuccess ||
+            mvxi_queue_stream(&g_hop.s[1], "MVX_STAGE_STREAM", "plain") != hipSuccess)
             return MPI_ERR_OTHER;
         for (b = 0; b < HOP_NB; b++)
             if (hipEventCreateWithFlags(&g_hop.ein[b], hipEventDisableTiming) != hipSuccess ||

@@ -48,6 +48,7 @@ int mvx_copy_threads(void);
  * registration cache on a pageable range of at least its minimum is
  * registered (or found registered) and reads as MVX_BUF_PINNED */
 MVXI int mvxi_buf_kind_range(const void *p, size_t bytes);
+MVXI hipError_t mvxi_queue_stream(hipStream_t *s, const char *env, const char *dflt);
 
 /* ---- errors (mvx_comm.c) ----------------------------------------------- */
 #define ERR_KIND_DEFAULT 1      /* MPIR_ERR_DEFAULT, mpi_error.h:119 */

@@ -34,8 +34,8 @@ static int stage_init(stage_res_t *R, size_t bounce)
 {
     int b;
     if (!R->ready) {
-        if (hipStreamCreateWithFlags(&R->sh, hipStreamNonBlocking) != hipSuccess ||
-            hipStreamCreateWithFlags(&R->sd, hipStreamNonBlocking) != hipSuccess)
+        if (mvxi_queue_stream(&R->sh, "MVX_STAGE_STREAM", "plain") != hipSuccess ||
+            mvxi_queue_stream(&R->sd, "MVX_STAGE_STREAM", "plain") != hipSuccess)
             return MPI_ERR_OTHER;
         for (b = 0; b < STAGE_NB; b++)
             if (hipEventCreateWithFlags(&R->ein[b], hipEventDisableTiming) != hipSuccess ||
