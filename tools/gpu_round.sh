@@ -3,7 +3,7 @@
 # trace, kernel micro-benches, host-buffer rates.  Every GPU step has its own
 # time limit; the chain stops at the first failure (no retries).
 #   tools/gpu_round.sh STAGE [pytest args]   (STAGE: all smoke test bench pmc prof kernels host
-#   bench_ab kernels_ab pmc_kernels rccl_net)
+#   bench_ab kernels_ab pmc_kernels rccl_net overlap)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
@@ -81,4 +81,9 @@ if [[ $STAGE == rccl_net ]]; then
   TRANSPORT=rccl-net tools/rehearse_full.sh c3 c4 || exit 1
   MVX_MP_CASES=${MVX_MP_CASES:-300} tools/rccl_net_sweep.sh > gpurun_out/rccl_net_sweep.jsonl || { cat gpurun_out/rccl_net_sweep.jsonl; exit 1; }
   cat gpurun_out/rccl_net_sweep.jsonl
+fi
+if [[ $STAGE == overlap ]]; then
+  # PIPE's combines under RCCL's transfers (kernel traces, p = 2 over rccl-net)
+  bash tools/prof_pipe_overlap.sh > gpurun_out/overlap.jsonl 2> gpurun_out/overlap.err || { tail -20 gpurun_out/overlap.err; exit 1; }
+  cat gpurun_out/overlap.jsonl
 fi
