@@ -279,12 +279,16 @@ int mvxi_job_layout(mvx_comm_t *c, rank_exec_t *X, const job_t *J, const mvx_pla
 /* The combine stream needs a hardware queue of its own (mvxi_queue_stream):
  * on a shared queue slice t + 1's transfers waited behind slice t's combine
  * (round 4, tools/prof_pipe_overlap.sh: 0.1 % of the combine time under a
- * transfer; 75 % of it with 4 slices on a queue of its own). */
+ * transfer; 75-78 % of it with 4 slices on a queue of its own).  The queue
+ * comes from a full CU mask rather than a raised priority: at equal
+ * priority the dispatcher serves the transfer kernel's few workgroups
+ * between the combine's, where a high-priority combine grid would be
+ * dispatched whole first. */
 static int pipe_streams(mvx_comm_t *c)
 {
     int i;
     if (c->cstream) return MPI_SUCCESS;
-    if (mvxi_queue_stream(&c->cstream, "MVX_PIPE_STREAM", "priority") != hipSuccess) return MPI_ERR_OTHER;
+    if (mvxi_queue_stream(&c->cstream, "MVX_PIPE_STREAM", "cumask") != hipSuccess) return MPI_ERR_OTHER;
     for (i = 0; i < 4; i++)
         if (hipEventCreateWithFlags(&c->pev[i], hipEventDisableTiming) != hipSuccess) return MPI_ERR_OTHER;
     return MPI_SUCCESS;

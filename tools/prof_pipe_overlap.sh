@@ -13,5 +13,5 @@ for ex in ${EXCHS:-p2p pipe}; do
   wait || exit 1
   f=$(find gpurun_out/prof_ov_${ex}_r0 -name "*kernel_trace.csv" | head -1)
   [ -n "$f" ] || exit 1
-  python3 tools/overlap.py "$f" "$ex ${MVX_PIPE_STREAM:-priority}" || exit 1
+  python3 tools/overlap.py "$f" "$ex ${MVX_PIPE_STREAM:-default}" || exit 1
 done
