@@ -322,14 +322,19 @@ hipError_t mvxi_queue_stream(hipStream_t *s, const char *env, const char *dflt)
     const char *e = getenv(env);
     int least = 0, greatest = 0;
     if (!e) e = dflt;
+    /* each flavour falls back to the next one if the runtime refuses it */
     if (!strcmp(e, "cumask")) {
         uint32_t mask[16];
         memset(mask, 0xff, sizeof mask);        /* 512 CUs: more than any part has */
-        return hipExtStreamCreateWithCUMask(s, 16, mask);
-    }
-    if (strcmp(e, "priority") || hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) {
+        if (hipExtStreamCreateWithCUMask(s, 16, mask) == hipSuccess) return hipSuccess;
         (void)hipGetLastError();
-        return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+        e = "priority";
     }
-    return hipStreamCreateWithPriority(s, hipStreamNonBlocking, greatest);
+    if (!strcmp(e, "priority")) {
+        if (hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess &&
+            hipStreamCreateWithPriority(s, hipStreamNonBlocking, greatest) == hipSuccess)
+            return hipSuccess;
+        (void)hipGetLastError();
+    }
+    return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
 }
