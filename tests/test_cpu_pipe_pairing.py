@@ -59,8 +59,13 @@ def _schedule(P, p, ns):
 
 
 def _cases(n_cases, seed):
+    """collective, p, count, recvcnts, op, type, root, slices, and the op
+    kind (predefined, or a user op: commutative / not, which the reference
+    sends through other algorithms) and the device flavour (ch_shmem or an
+    _SMP_ build's knobs, mvx_tuning_from_env)"""
     rng = np.random.default_rng(seed)
     kinds = [mvx.COLL_ALLREDUCE, mvx.COLL_REDUCE, mvx.COLL_REDUCE_SCATTER, mvx.COLL_SCAN]
+    smp = mvx.tuning_from_env(True)
     for _ in range(n_cases):
         p = int(rng.integers(2, 17))
         kind = kinds[int(rng.integers(0, len(kinds)))]
@@ -68,19 +73,22 @@ def _cases(n_cases, seed):
         dtype = 10
         root = int(rng.integers(0, p))
         ns = int(rng.integers(2, 9))
+        opkind = [None, mvx.OPKIND_USER_COMMUTE, mvx.OPKIND_USER_NONCOMMUTE][int(rng.integers(0, 3))]
+        tuning = smp if rng.integers(0, 4) == 0 else None
         if kind == mvx.COLL_REDUCE_SCATTER:
             cnts = [int(rng.integers(0, 60000)) for _ in range(p)]
-            yield kind, p, sum(cnts), cnts, op, dtype, root, ns
+            yield kind, p, sum(cnts), cnts, op, dtype, root, ns, opkind, tuning
         else:
-            yield kind, p, int(rng.integers(1, 500000)), None, op, dtype, root, ns
+            yield kind, p, int(rng.integers(1, 500000)), None, op, dtype, root, ns, opkind, tuning
 
 
 @pytest.mark.parametrize("seed", [1, 2, 3])
 def test_pipe_messages_pair_up(seed):
     checked = 0
-    for kind, p, n, cnts, op, dtype, root, ns in _cases(150, seed):
+    for kind, p, n, cnts, op, dtype, root, ns, opkind, tuning in _cases(150, seed):
         try:
-            plans = [mvx.plan(kind, p, r, n, dtype, op, root=root, recvcnts=cnts) for r in range(p)]
+            plans = [mvx.plan(kind, p, r, n, dtype, op, root=root, recvcnts=cnts, opkind=opkind, tuning=tuning)
+                     for r in range(p)]
         except ValueError:
             continue
         sched = [_schedule(P, p, ns) for P in plans]
