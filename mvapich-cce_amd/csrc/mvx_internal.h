@@ -196,8 +196,8 @@ typedef struct mvx_work {
     graph_ent_t graphs[GRAPH_CACHE];           /* captured device calls */
     unsigned long graph_clock;
     mvx_plan call_plan;                        /* mvx_api.c run(): this rank's plan */
-    mvx_plan pipe[3][MVX_MAXP];                /* PIPE: slice plans (two in use) */
-    rank_exec_t px0[MVX_MAXP], px[3][MVX_MAXP];
+    mvx_plan pipe[2][MVX_MAXP];                /* PIPE: slice plans, by slice parity */
+    rank_exec_t px0[MVX_MAXP], px[2][MVX_MAXP];
     mvx_plan slice[2][MVX_MAXP];               /* staged: current and previous slice */
     job_t pk_job;                              /* packed datatypes */
     packed_bufs_t pk_bufs;
