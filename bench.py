@@ -198,6 +198,50 @@ def _rc_of(rc):
     return 128 - rc if rc < 0 else rc      # a signal -> 128 + signo, as a shell reports it
 
 
+KFD_NODES = "/sys/class/kfd/kfd/topology/nodes"
+
+
+def visible_gpus(env=None, nodes=None):
+    """GPUs this process may use, counted without HIP or torch: the KFD
+    topology's nodes with SIMDs (a CPU node has simd_count 0), narrowed by
+    ROCR_VISIBLE_DEVICES and then HIP_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES
+    (indices, or ROCr's GPU-<unique_id> names).  None when the topology
+    cannot be read (then nothing is checked before the workers start)."""
+    env = os.environ if env is None else env
+    nodes = nodes or env.get("MVX_KFD_NODES", KFD_NODES)
+    try:
+        names = sorted(os.listdir(nodes), key=lambda x: int(x) if x.isdigit() else 1 << 30)
+    except OSError:
+        return None
+    gpus = []
+    for name in names:
+        try:
+            with open(os.path.join(nodes, name, "properties")) as f:
+                props = dict(line.split(None, 1) for line in f if len(line.split(None, 1)) == 2)
+        except OSError:
+            continue
+        if int(props.get("simd_count", "0")) > 0:
+            gpus.append("GPU-%016x" % int(props.get("unique_id", "0")))
+
+    def narrow(ids, var):
+        v = env.get(var)
+        if v is None:
+            return ids
+        out = []
+        for e in (x.strip() for x in v.split(",")):
+            if e.isdigit() and int(e) < len(ids):
+                out.append(ids[int(e)])
+            elif e.upper().startswith("GPU-") and e.lower() in (i.lower() for i in ids):
+                out.append(e)
+            else:
+                break                      # the runtimes stop at the first invalid entry
+        return out
+
+    gpus = narrow(gpus, "ROCR_VISIBLE_DEVICES")
+    gpus = narrow(gpus, "HIP_VISIBLE_DEVICES" if "HIP_VISIBLE_DEVICES" in env else "CUDA_VISIBLE_DEVICES")
+    return len(gpus)
+
+
 def launch(args, n, argv):
     """--gpus N > 1 with no WORLD_SIZE: one worker process per GPU, started
     before this process touches the GPU (it never does), never by exec.
@@ -210,9 +254,8 @@ def launch(args, n, argv):
     import subprocess
     import threading
     if args.transport == "rccl":
-        import torch          # counting devices does not initialise the GPU
-        have = torch.cuda.device_count()
-        if have < n:
+        have = visible_gpus()     # no HIP call (and no torch) in this process
+        if have is not None and have < n:
             sys.stderr.write("bench: --gpus %d over RCCL needs %d GPUs, this box has %d (RCCL refuses two "
                              "ranks on one GPU; --transport rccl-net or host shares one)\n" % (n, n, have))
             return 2
@@ -1106,12 +1149,24 @@ def run_multi(args, mvx, dev, world, rank, local, clock):
         terr = 0
         if EXCH[name][2]:
             # graphs: each input set's first call ran eagerly, its second is
-            # captured -- untimed here, so the tuning steps are replays
+            # captured -- untimed here, so the tuning steps are replays.  A
+            # first launch that never completes is a hung variant like any
+            # other: a bounded wait, then agree / recover.
             try:
                 for _ in range(2 * sets):
                     step()
             except RuntimeError:
                 terr = 1
+            if terr == 0 and not _wait_stream(stream, step_limit(args, est)):
+                terr = 2
+            worst = agree(terr)
+            if worst:
+                entry.update(ms_per_step=None, parity=ok,
+                             error=("an error return on some rank while capturing" if worst == 1 else
+                                    "a captured step did not complete within %.0f s" % step_limit(args, est)))
+                recover(worst, entry)
+                clock.mark("variant %s" % name)
+                continue
         torch.cuda.synchronize()
         dist.barrier()
         t0 = time.perf_counter()

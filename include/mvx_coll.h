@@ -31,7 +31,9 @@ extern "C" {
 
 /* ---- communicators ----------------------------------------------------- */
 
-/* rank 0 creates the id, every rank passes the same bytes to mvx_comm_init */
+/* rank 0 creates the id, every rank passes the same bytes to mvx_comm_init.
+ * Creation and every call on a communicator switch to its device for their
+ * duration; the caller's current device is left as it was. */
 int mvx_get_unique_id(void *id_out);
 /* one process per GPU: collective over `size` processes (RCCL over xGMI);
  * the first communicator created becomes MPI_COMM_WORLD. */
@@ -232,21 +234,6 @@ int mvx_coll_scan(void *sendbuf, void *recvbuf, int count, MPI_Datatype datatype
                   MPI_Op op, MPI_Comm comm);
 /* 1 if p is device (or managed) memory the device path can use directly */
 int mvx_buffer_is_device(const void *p);
-
-/* Registration cache for pageable host buffers (MVAPICH's dreg,
- * mpid/ch_gen2/dreg.c:774-832): with it on, a pageable range a call uses is
- * page-locked (hipHostRegister) on first use and kept, so later calls DMA
- * it directly.  Off by default; MVX_HOST_REGISTER=1 turns it on,
- * MVX_HOST_REGISTER_MAX_MIB (16384) caps the registered bytes (least
- * recently used entries are dropped), MVX_HOST_REGISTER_MIN_KIB (1024) is
- * the smallest range registered.  Contract: call mvx_host_unregister(addr)
- * for a registered buffer before freeing it (the reference's mem_hooks.c
- * does this from malloc hooks).  max_bytes 0 keeps the current cap; turning
- * the cache off drops every registration. */
-int mvx_host_register_enable(int on, size_t max_bytes);
-/* Drops every registration containing addr: 0, or MPI_ERR_ARG if none. */
-int mvx_host_unregister(const void *addr);
-int mvx_host_register_stats(long *entries, size_t *bytes, long *hits, long *misses);
 
 int PMPI_Reduce(void *, void *, int, MPI_Datatype, MPI_Op, int, MPI_Comm);
 int PMPI_Allreduce(void *, void *, int, MPI_Datatype, MPI_Op, MPI_Comm);

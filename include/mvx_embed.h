@@ -24,11 +24,19 @@ extern "C" {
 
 #define MVX_UNIQUE_ID_BYTES 128
 
-/* communicators: one process per GPU, collective over `size` processes */
+/* communicators: one process per GPU, collective over `size` processes.
+ * Creation and every call on a communicator run on its device and leave the
+ * caller's current device as it was. */
 int mvx_get_unique_id(void *id_out);
 int mvx_comm_init(int *comm, int rank, int size, int device, const void *unique_id);
 int mvx_comm_free(int *comm);
+/* teardown without waiting for peers (ncclCommAbort; mvx_coll.h) */
+int mvx_comm_abort(int *comm);
 int mvx_device_count(void);
+/* 0 if `device` can be selected and given a context -- what mvx_comm_init
+ * needs of this rank before it enters RCCL's collective creation; 15
+ * (MPI_ERR_OTHER) otherwise.  The current device is kept. */
+int mvx_device_check(int device);
 /* 1 if p is device (or managed) memory */
 int mvx_buffer_is_device(const void *p);
 
@@ -54,6 +62,43 @@ int mvx_op_free(int *op);
  * intra_fns_new.c:5697).  handle == type removes the mapping.  Returns 0, or
  * MPI_ERR_OTHER (15) when the table (256 entries) is full. */
 int mvx_type_set_handle(int type, int handle);
+
+/* Registration cache for pageable host buffers (MVAPICH's dreg,
+ * mpid/ch_gen2/dreg.c:774-832): with it on, a pageable range a call uses is
+ * page-locked (hipHostRegister) on first use and kept, so later calls DMA
+ * it directly.  A registration must never outlive its memory (a DMA through
+ * one whose pages were freed and mapped again faults the GPU), so the cache
+ * drops every registration inside a range before that range is released:
+ *   on = 1  libmvx.so's release hooks report releases (free, realloc,
+ *           munmap, mremap, madvise DONTNEED/FREE/REMOVE, negative sbrk are
+ *           interposed, as the reference's mem_hooks.c interposes munmap and
+ *           sbrk).  They are in effect when libmvx.so is in the program's
+ *           global scope ahead of libc (a program linked with -lmvx);
+ *           mvx_host_hooks_active says whether they are.  Without them
+ *           on = 1 is refused (MPI_ERR_OTHER) and the cache stays off.
+ *   on = 2  the caller reports releases: mvx_host_unregister(addr) before it
+ *           frees a buffer it passed, or mvx_host_invalidate(addr, bytes)
+ *           from its own memory hooks (a host MPI's mem_hooks.c;
+ *           libmvx_embed.so has no hooks of its own).
+ *   on = 0  off: every registration is dropped.
+ * Env at first use: MVX_HOST_REGISTER=1|2 (1 only where the hooks are in
+ * effect), MVX_HOST_REGISTER_MAX_MIB (16384) caps the registered bytes
+ * (least recently used entries are dropped), MVX_HOST_REGISTER_MIN_KIB
+ * (1024) is the smallest range registered.  max_bytes 0 keeps the cap. */
+int mvx_host_register_enable(int on, size_t max_bytes);
+int mvx_host_hooks_active(void);
+/* Registers [addr, addr + bytes) now (as a call using it would): 0, or
+ * MPI_ERR_OTHER (cache off, range below the minimum, refused). */
+int mvx_host_register(const void *addr, size_t bytes);
+/* Drops every registration containing addr: 0, or MPI_ERR_ARG if none. */
+int mvx_host_unregister(const void *addr);
+/* Drops every registration overlapping [addr, addr + bytes), which is about
+ * to be released (the reference's find_and_free_dregs_inside, dreg.c:1063):
+ * the number dropped. */
+int mvx_host_invalidate(const void *addr, size_t bytes);
+int mvx_host_register_stats(long *entries, size_t *bytes, long *hits, long *misses);
+/* registrations dropped by releases (hooks and mvx_host_invalidate) so far */
+long mvx_host_register_invalidations(void);
 
 /* device flavour and collective knobs (the reference's _SMP_ collops) */
 typedef struct mvx_tuning {

@@ -1,5 +1,5 @@
-/* harness.c -- TEST HELPER: a one-process stand-in for the MPICH runtime
- * calls integration/intra_mvx.c makes (MPIR_ToPointer, attributes,
+/* harness.c -- TEST HELPER: a stand-in for the MPICH runtime calls
+ * integration/intra_mvx.c makes (MPIR_ToPointer, attributes,
  * MPIR_intra_collops, MPIR_COMM_WORLD), so tests/test_cpu_integration.py and
  * tests/test_gpu_integration.py can drive the shim's collops table through
  * ctypes.  Compile-check headers: integration/check/README.md.
@@ -7,9 +7,20 @@
  * Datatype nodes are built the way the reference's constructors store them
  * (field values supplied by the test from the oracle's restated bounds);
  * MPIR_intra_collops, standing for MVAPICH's own (host) path, counts its
- * calls and, for a one-rank communicator, copies sendbuf to recvbuf. */
+ * calls and, for a one-rank communicator, copies sendbuf to recvbuf.
+ *
+ * World of np processes (h_init_world): each process is one rank of
+ * MPI_COMM_WORLD; the stand-in's Bcast and its Allreduce of a few MPI_INTs
+ * (the shim's route and creation agreements, counted apart from the data
+ * calls) move their bytes through a board in a file every rank maps, with a
+ * time limit so a rank that never arrives fails the call instead of hanging
+ * the test. */
 #include <stdlib.h>
 #include <string.h>
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <time.h>
+#include <unistd.h>
 
 #include "mpiimpl.h"
 #include "mpiops.h"
@@ -98,9 +109,51 @@ int h_comm_free_attrs(int comm)
 }
 
 /* ---- the host path ("MVAPICH's own") ------------------------------------ */
-static int g_host_calls;
+static int g_host_calls, g_agree_calls;
 static struct MPIR_COMMUNICATOR g_world;
 struct MPIR_COMMUNICATOR *MPIR_COMM_WORLD = &g_world;
+
+/* the board: slot[r][g & 1] holds rank r's bytes of exchange g; arrive[r] =
+ * the last exchange rank r has written.  Double-buffered by parity: a rank
+ * writing exchange g + 2 has seen every rank arrive at g + 1, so each has
+ * read exchange g. */
+#define BOARD_RANKS 16
+#define BOARD_SLOT 256
+typedef struct {
+    volatile long arrive[BOARD_RANKS];
+    char slot[BOARD_RANKS][2][BOARD_SLOT];
+} board_t;
+static board_t *g_board;
+static long g_gen;
+static double g_limit_s = 60.0;
+
+static double now_s(void)
+{
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return (double)t.tv_sec + 1e-9 * (double)t.tv_nsec;
+}
+
+/* every rank's `bytes` (<= BOARD_SLOT) of this exchange into out[r * bytes] */
+static int board_allgather(const void *mine, int bytes, void *out)
+{
+    const int np = g_world.np, me = g_world.local_rank;
+    const long g = ++g_gen;
+    const double t0 = now_s();
+    int r;
+    if (!g_board || bytes > BOARD_SLOT) return MPI_ERR_OTHER;
+    memcpy(g_board->slot[me][g & 1], mine, (size_t)bytes);
+    __atomic_store_n(&g_board->arrive[me], g, __ATOMIC_RELEASE);
+    for (r = 0; r < np; r++) {
+        while (__atomic_load_n(&g_board->arrive[r], __ATOMIC_ACQUIRE) < g) {
+            struct timespec ts = {0, 200000};
+            if (now_s() - t0 > g_limit_s) return MPI_ERR_OTHER;
+            nanosleep(&ts, NULL);
+        }
+        memcpy((char *)out + (size_t)r * bytes, g_board->slot[r][g & 1], (size_t)bytes);
+    }
+    return MPI_SUCCESS;
+}
 
 static void host_copy(void *s, void *r, long n, struct MPIR_DATATYPE *d)
 {
@@ -108,8 +161,35 @@ static void host_copy(void *s, void *r, long n, struct MPIR_DATATYPE *d)
 }
 static int host_bcast(void *b, int n, struct MPIR_DATATYPE *d, int root, struct MPIR_COMMUNICATOR *c)
 {
-    (void)b; (void)n; (void)d; (void)root;
-    return c->np == 1 ? MPI_SUCCESS : MPI_ERR_OTHER;
+    char all[BOARD_RANKS * BOARD_SLOT];
+    const long bytes = (long)n * d->extent;
+    if (c->np == 1) return MPI_SUCCESS;
+    if (bytes > BOARD_SLOT || board_allgather(b, (int)bytes, all)) return MPI_ERR_OTHER;
+    memcpy(b, all + (size_t)root * (size_t)bytes, (size_t)bytes);
+    return MPI_SUCCESS;
+}
+
+/* the shim's agreements: an Allreduce of at most 4 MPI_INTs with MPI_MAX or
+ * MPI_MIN, reduced for real across the world's ranks */
+static int agreement(int n, struct MPIR_DATATYPE *d, MPI_Op op)
+{
+    return d->self == MPI_INT && n >= 1 && n <= 4 && (op == MPI_MAX || op == MPI_MIN);
+}
+
+static int host_agree(const int *s, int *r, int n, MPI_Op op, struct MPIR_COMMUNICATOR *c)
+{
+    int all[BOARD_RANKS * 4], i, q;
+    g_agree_calls++;
+    if (c->np == 1) { memcpy(r, s, (size_t)n * sizeof(int)); return MPI_SUCCESS; }
+    if (board_allgather(s, n * (int)sizeof(int), all)) return MPI_ERR_OTHER;
+    for (i = 0; i < n; i++) {
+        r[i] = all[i];
+        for (q = 1; q < c->np; q++) {
+            const int v = all[q * n + i];
+            if (op == MPI_MAX ? v > r[i] : v < r[i]) r[i] = v;
+        }
+    }
+    return MPI_SUCCESS;
 }
 static int host_reduce(void *s, void *r, int n, struct MPIR_DATATYPE *d, MPI_Op op, int root,
                     struct MPIR_COMMUNICATOR *c)
@@ -122,7 +202,7 @@ static int host_reduce(void *s, void *r, int n, struct MPIR_DATATYPE *d, MPI_Op 
 static int host_allreduce(void *s, void *r, int n, struct MPIR_DATATYPE *d, MPI_Op op,
                        struct MPIR_COMMUNICATOR *c)
 {
-    (void)op; (void)c;
+    if (agreement(n, d, op)) return host_agree((const int *)s, (int *)r, n, op, c);
     g_host_calls++;
     host_copy(s, r, n, d);
     return MPI_SUCCESS;
@@ -143,17 +223,49 @@ MPIR_COLLOPS MPIR_intra_collops = &g_intra;
 MPIR_COLLOPS MPIR_inter_collops = &g_intra;
 
 int h_host_calls(void) { return g_host_calls; }
+int h_agree_calls(void) { return g_agree_calls; }
 
 #ifdef HARNESS_SMP
 int enable_shmem_collectives = 1;     /* src/env/initutil.c:146 */
 #endif
 MPI_Fint MPIR_F_TRUE = 1, MPIR_F_FALSE = 0;   /* initfutil.c:100, gfortran's literals */
 
+static int the_world(int rank, int np);
+
 /* one-rank world, the shim's table installed */
-int h_init(void)
+int h_init(void) { return the_world(0, 1); }
+
+/* rank `rank` of an np-process world whose board is the file `path` (every
+ * rank passes the same path; the test creates it, zero-filled, beforehand);
+ * limit_s bounds each board exchange */
+int h_init_world(int rank, int np, const char *path, double limit_s)
 {
-    g_world.np = 1;
-    g_world.local_rank = 0;
+    int fd;
+    void *m;
+    if (np < 1 || np > BOARD_RANKS || rank < 0 || rank >= np) return 1;
+    fd = open(path, O_RDWR);
+    if (fd < 0) return 1;
+    if (ftruncate(fd, sizeof(board_t))) { close(fd); return 1; }
+    m = mmap(NULL, sizeof(board_t), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    close(fd);
+    if (m == MAP_FAILED) return 1;
+    g_board = (board_t *)m;
+    if (limit_s > 0) g_limit_s = limit_s;
+    return the_world(rank, np);
+}
+
+static int the_world(int rank, int np)
+{
+    /* the predefined types the shim's own calls name (MPI_INT, MPI_BYTE) */
+    static struct MPIR_DATATYPE t_int, t_byte;
+    t_int.dte_type = MPIR_INT; t_int.basic = t_int.permanent = 1; t_int.self = MPI_INT;
+    t_int.extent = t_int.ub = t_int.size = 4;
+    t_byte.dte_type = MPIR_BYTE; t_byte.basic = t_byte.permanent = 1; t_byte.self = MPI_BYTE;
+    t_byte.extent = t_byte.ub = t_byte.size = 1;
+    if (!g_ptr[MPI_INT]) g_ptr[MPI_INT] = &t_int;
+    if (!g_ptr[MPI_BYTE]) g_ptr[MPI_BYTE] = &t_byte;
+    g_world.np = np;
+    g_world.local_rank = rank;
     g_world.self = 91;             /* MPI_COMM_WORLD, mpi.h:119 */
     g_world.comm_type = 1;         /* MPIR_INTRA */
     g_world.comm_coll = &g_world;

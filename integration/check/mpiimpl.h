@@ -18,7 +18,9 @@ typedef int MPI_Fint;                          /* mpidefs.h.in:9 */
 #define MPI_ERR_EXHAUSTED (MPI_ERR_INTERN | (1 << 6))   /* mpi_error.h:249 */
 
 #define MPI_BYTE          ((MPI_Datatype)3)    /* mpi.h:67 */
+#define MPI_INT           ((MPI_Datatype)6)    /* mpi.h:70 */
 #define MPI_MAX           (MPI_Op)(100)        /* mpi.h:129 */
+#define MPI_MIN           (MPI_Op)(101)        /* mpi.h:130 */
 #define MPI_MAXLOC        (MPI_Op)(111)        /* mpi.h:140 */
 #define MPI_KEYVAL_INVALID 0                   /* mpi.h:170 */
 

@@ -10,9 +10,10 @@
  *
  * The table is MPIR_intra_collops (include/mpicoll.h:59) with Reduce,
  * Allreduce, Reduce_scatter and Scan replaced.  Each replacement sends a call
- * whose buffers are device memory (or every call, with MVX_HOST_BUFFERS=1)
- * to libmvx, which computes the reference's bits in the reference's combine
- * order; anything else runs MVAPICH's own function unchanged.
+ * in which some rank's buffers are device memory (or every call, with
+ * MVX_HOST_BUFFERS=1) to libmvx on every rank, which computes the
+ * reference's bits in the reference's combine order; a call with host
+ * buffers on every rank runs MVAPICH's own function unchanged (Route below).
  *
  * What it reads of the reference's objects (nothing is added to them):
  *   struct MPIR_COMMUNICATOR  np, local_rank, self        mpid/ch2/comm.h:65-113
@@ -28,11 +29,36 @@
  * with a delete callback, src/context/keyvalcreate.c:57), so MPI_Comm_free
  * releases the libmvx communicator.
  *
+ * Route (one per call, the same on every rank).  MPI lets ranks pass
+ * buffers of different kinds to one call, and every algorithm assumes all
+ * ranks run the same function (comm_util.c:321-331 installs one table per
+ * communicator; intra_fns_new.c:5453), so the choice between libmvx and
+ * MVAPICH's own function is agreed, never taken rank-locally:
+ *   MVX_SHIM_ROUTE=agree (default)  one MPIR_intra_collops->Allreduce of two
+ *                 ints (MPI_MAX of {device buffers here, host buffers here})
+ *                 on the host path: if any rank passes device memory (or sets
+ *                 MVX_HOST_BUFFERS=1) every rank calls libmvx -- a host-buffer
+ *                 rank through libmvx's host staging -- otherwise every rank
+ *                 runs MVAPICH's function.  Skipped at np == 1 and for an
+ *                 empty call (count 0 on every rank, as MPI requires).
+ *   MVX_SHIM_ROUTE=local   no agreement: the caller promises every rank's
+ *                 buffers agree in kind in every call (the route is this
+ *                 rank's own buffer test).
+ *   MVX_SHIM_ROUTE must be the same on every rank, like any MVAPICH knob.
+ *
  * Translation, per call, cached:
- *   communicator  the first reduction on a communicator creates its libmvx
- *                 twin collectively: rank 0's mvx_get_unique_id is broadcast
- *                 with MVAPICH's own Bcast, then mvx_comm_init(local_rank,
- *                 np, device).  device = $MVX_DEVICE_ID, else the
+ *   communicator  the first call routed to libmvx creates the twin, on every
+ *                 rank together (the route is agreed): each rank checks its
+ *                 device (mvx_device_check), rank 0 makes the RCCL id; an
+ *                 MPI_MIN Allreduce agrees that all of it worked before any
+ *                 rank enters RCCL's collective creation (a rank that cannot
+ *                 would leave its peers in ncclCommInitRank for good); the id
+ *                 is broadcast with MVAPICH's own Bcast; mvx_comm_init(
+ *                 local_rank, np, device); a second MIN agrees creation
+ *                 succeeded everywhere (ranks that got one abort it
+ *                 otherwise).  A failure is recorded on every rank alike:
+ *                 every later call routed to libmvx returns MPI_ERR_OTHER on
+ *                 every rank.  device = $MVX_DEVICE_ID, else the
  *                 MPI_COMM_WORLD rank modulo the visible GPUs.
  *   datatype      a permanent type's handle is libmvx's handle (the values
  *                 of include/mpi.h:64-140); a derived type is rebuilt from
@@ -53,10 +79,7 @@
  *                 (intra_fns_new.c:4992-5198, 5793-5940).  libmvx models one
  *                 node: a communicator spanning nodes (leader_comm size > 1)
  *                 is planned without the shmem step.
- *
- * Buffers on different ranks must agree on device vs host memory (as with
- * any GPU-aware MPI); a rank with host buffers takes MVAPICH's path, a rank
- * with device buffers libmvx's.
+
  */
 #include <stdlib.h>
 #include <string.h>
@@ -120,12 +143,56 @@ static void shim_tuning(int h, struct MPIR_COMMUNICATOR *comm)
     mvx_comm_set_tuning(h, &t);
 }
 
-/* the libmvx twin of `comm`, created collectively on first use; -1 if none */
+/* MPI_MIN of `v` over the communicator (MVAPICH's own Allreduce); 0 if it
+ * fails, so a broken agreement reads as "not everywhere" */
+static int agree_min(int v, struct MPIR_COMMUNICATOR *comm)
+{
+    int all = 0;
+    if (MPIR_intra_collops->Allreduce(&v, &all, 1, MPIR_GET_DTYPE_PTR(MPI_INT), MPI_MIN, comm) !=
+        MPI_SUCCESS)
+        return 0;
+    return all;
+}
+
+/* create the twin on every rank together; s->mvx = handle, or -1 on every
+ * rank when any rank could not take part */
+static void twin_create(mvx_shim_comm *s, struct MPIR_COMMUNICATOR *comm)
+{
+    char id[MVX_UNIQUE_ID_BYTES];
+    const int dev = shim_device();
+    int ok;
+
+    s->mvx = -1;
+    memset(id, 0, sizeof id);
+    /* this rank can enter RCCL's creation: a usable device, and rank 0 an id */
+    ok = mvx_device_check(dev) == 0;
+    if (ok && comm->local_rank == 0) ok = mvx_get_unique_id(id) == 0;
+    if (!agree_min(ok, comm)) return;
+    if (MPIR_intra_collops->Bcast(id, MVX_UNIQUE_ID_BYTES, MPIR_GET_DTYPE_PTR(MPI_BYTE), 0, comm) !=
+        MPI_SUCCESS)
+        ok = 0;
+    if (ok && mvx_comm_init(&s->mvx, comm->local_rank, comm->np, dev, id) != 0) {
+        s->mvx = -1;
+        ok = 0;
+    }
+    if (!agree_min(ok, comm)) {
+        if (s->mvx >= 0) mvx_comm_abort(&s->mvx);
+        s->mvx = -1;
+        return;
+    }
+    shim_tuning(s->mvx, comm);
+#ifndef MPID_NO_FORTRAN
+    /* MPI_LOGICAL's words, as mpir_init_flog set them (initfutil.c:189) */
+    mvx_set_fortran_logical(MPIR_F_TRUE, MPIR_F_FALSE);
+#endif
+}
+
+/* the libmvx twin of `comm`, created on first use by every rank together
+ * (callers reach here only on an agreed route); -1 if creation failed */
 static int shim_comm(struct MPIR_COMMUNICATOR *comm)
 {
     mvx_shim_comm *s = NULL;
-    char id[MVX_UNIQUE_ID_BYTES];
-    int flag = 0, rc;
+    int flag = 0;
 
     if (g_keyval == MPI_KEYVAL_INVALID &&
         MPI_Keyval_create(MPI_NULL_COPY_FN, shim_delete, &g_keyval, NULL) != MPI_SUCCESS)
@@ -135,20 +202,7 @@ static int shim_comm(struct MPIR_COMMUNICATOR *comm)
 
     s = (mvx_shim_comm *)malloc(sizeof *s);
     if (!s) return -1;
-    memset(id, 0, sizeof id);
-    if (comm->local_rank == 0) mvx_get_unique_id(id);
-    rc = MPIR_intra_collops->Bcast(id, MVX_UNIQUE_ID_BYTES, MPIR_GET_DTYPE_PTR(MPI_BYTE), 0, comm);
-    if (rc != MPI_SUCCESS ||
-        mvx_comm_init(&s->mvx, comm->local_rank, comm->np, shim_device(), id) != 0) {
-        s->mvx = -1;
-    } else {
-        shim_tuning(s->mvx, comm);
-#ifndef MPID_NO_FORTRAN
-        /* MPI_LOGICAL's words, as mpir_init_flog set them (initfutil.c:189),
-           on the device mvx_comm_init made current */
-        mvx_set_fortran_logical(MPIR_F_TRUE, MPIR_F_FALSE);
-#endif
-    }
+    twin_create(s, comm);
     MPI_Attr_put(comm->self, g_keyval, s);
     return s->mvx;
 }
@@ -346,11 +400,34 @@ int mvx_shim_op(MPI_Op op, int *out)
 
 /* ---- the collops members ------------------------------------------------ */
 
-static int on_gpu(const void *sendbuf, const void *recvbuf)
+/* this rank's wish: 1 for libmvx (device memory, or MVX_HOST_BUFFERS=1) */
+static int wants_mvx(const void *sendbuf, const void *recvbuf)
 {
     const char *e = getenv("MVX_HOST_BUFFERS");
     if (e && atoi(e) == 1) return 1;
     return mvx_buffer_is_device(sendbuf) || mvx_buffer_is_device(recvbuf);
+}
+
+static int route_local(void)
+{
+    const char *e = getenv("MVX_SHIM_ROUTE");
+    return e && !strcmp(e, "local");
+}
+
+/* The route of one call, the same on every rank: 1 libmvx, 0 MVAPICH's own
+ * function; `empty` (no element on any rank) needs no agreement.  A failed
+ * agreement returns -1 with *rc set. */
+static int route(const void *sendbuf, const void *recvbuf, int empty, struct MPIR_COMMUNICATOR *comm,
+                 int *rc)
+{
+    int v[2], all[2];
+    const int mine = wants_mvx(sendbuf, recvbuf);
+    if (empty || comm->np == 1 || route_local()) return mine && !empty;
+    v[0] = mine;
+    v[1] = !mine;
+    *rc = MPIR_intra_collops->Allreduce(v, all, 2, MPIR_GET_DTYPE_PTR(MPI_INT), MPI_MAX, comm);
+    if (*rc != MPI_SUCCESS) return -1;
+    return all[0] != 0;
 }
 
 /* communicator, datatype and op in libmvx's handles */
@@ -358,18 +435,19 @@ static int translate(struct MPIR_COMMUNICATOR *comm, struct MPIR_DATATYPE *dt, M
                      int *h, int *t, int *o)
 {
     int rc;
+    /* the communicator first: its creation is collective, the rest local */
+    if ((*h = shim_comm(comm)) < 0) return MPI_ERR_OTHER;
     if ((rc = mvx_shim_type(dt, t))) return rc;
-    if ((rc = mvx_shim_op(op, o))) return rc;
-    *h = shim_comm(comm);
-    return *h < 0 ? MPI_ERR_OTHER : MPI_SUCCESS;
+    return mvx_shim_op(op, o);
 }
 
 static int mvx_Reduce(void *sendbuf, void *recvbuf, int count, struct MPIR_DATATYPE *dt, MPI_Op op,
                       int root, struct MPIR_COMMUNICATOR *comm)
 {
-    int h, t, o, rc;
-    if (!on_gpu(sendbuf, recvbuf))
-        return MPIR_intra_collops->Reduce(sendbuf, recvbuf, count, dt, op, root, comm);
+    int h, t, o, rc = MPI_SUCCESS;
+    const int r = route(sendbuf, recvbuf, count == 0, comm, &rc);
+    if (r < 0) return rc;
+    if (!r) return MPIR_intra_collops->Reduce(sendbuf, recvbuf, count, dt, op, root, comm);
     if ((rc = translate(comm, dt, op, &h, &t, &o))) return rc;
     return mvx_coll_reduce(sendbuf, recvbuf, count, t, o, root, h);
 }
@@ -377,9 +455,10 @@ static int mvx_Reduce(void *sendbuf, void *recvbuf, int count, struct MPIR_DATAT
 static int mvx_Allreduce(void *sendbuf, void *recvbuf, int count, struct MPIR_DATATYPE *dt,
                          MPI_Op op, struct MPIR_COMMUNICATOR *comm)
 {
-    int h, t, o, rc;
-    if (!on_gpu(sendbuf, recvbuf))
-        return MPIR_intra_collops->Allreduce(sendbuf, recvbuf, count, dt, op, comm);
+    int h, t, o, rc = MPI_SUCCESS;
+    const int r = route(sendbuf, recvbuf, count == 0, comm, &rc);
+    if (r < 0) return rc;
+    if (!r) return MPIR_intra_collops->Allreduce(sendbuf, recvbuf, count, dt, op, comm);
     if ((rc = translate(comm, dt, op, &h, &t, &o))) return rc;
     return mvx_coll_allreduce(sendbuf, recvbuf, count, t, o, h);
 }
@@ -387,9 +466,11 @@ static int mvx_Allreduce(void *sendbuf, void *recvbuf, int count, struct MPIR_DA
 static int mvx_Reduce_scatter(void *sendbuf, void *recvbuf, int *recvcnts,
                               struct MPIR_DATATYPE *dt, MPI_Op op, struct MPIR_COMMUNICATOR *comm)
 {
-    int h, t, o, rc;
-    if (!on_gpu(sendbuf, recvbuf))
-        return MPIR_intra_collops->Reduce_scatter(sendbuf, recvbuf, recvcnts, dt, op, comm);
+    int h, t, o, r, rc = MPI_SUCCESS, i, empty = 1;
+    for (i = 0; i < comm->np && recvcnts; i++) empty &= recvcnts[i] == 0;  /* same counts everywhere */
+    r = route(sendbuf, recvbuf, empty, comm, &rc);
+    if (r < 0) return rc;
+    if (!r) return MPIR_intra_collops->Reduce_scatter(sendbuf, recvbuf, recvcnts, dt, op, comm);
     if ((rc = translate(comm, dt, op, &h, &t, &o))) return rc;
     return mvx_coll_reduce_scatter(sendbuf, recvbuf, recvcnts, t, o, h);
 }
@@ -397,9 +478,10 @@ static int mvx_Reduce_scatter(void *sendbuf, void *recvbuf, int *recvcnts,
 static int mvx_Scan(void *sendbuf, void *recvbuf, int count, struct MPIR_DATATYPE *dt, MPI_Op op,
                     struct MPIR_COMMUNICATOR *comm)
 {
-    int h, t, o, rc;
-    if (!on_gpu(sendbuf, recvbuf))
-        return MPIR_intra_collops->Scan(sendbuf, recvbuf, count, dt, op, comm);
+    int h, t, o, rc = MPI_SUCCESS;
+    const int r = route(sendbuf, recvbuf, count == 0, comm, &rc);
+    if (r < 0) return rc;
+    if (!r) return MPIR_intra_collops->Scan(sendbuf, recvbuf, count, dt, op, comm);
     if ((rc = translate(comm, dt, op, &h, &t, &o))) return rc;
     return mvx_coll_scan(sendbuf, recvbuf, count, t, o, h);
 }

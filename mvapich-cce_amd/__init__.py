@@ -140,6 +140,10 @@ def _load():
     c.mvx_comm_reap.argtypes = []
     c.mvx_host_register_enable.argtypes = [i, sz]
     c.mvx_host_unregister.argtypes = [vp]
+    c.mvx_host_invalidate.argtypes = [vp, sz]
+    c.mvx_host_register.argtypes = [vp, sz]
+    c.mvx_host_hooks_active.argtypes = []
+    c.mvx_host_register_invalidations.restype = ctypes.c_long
     c.mvx_host_register_stats.argtypes = [ctypes.POINTER(ctypes.c_long), ctypes.POINTER(ctypes.c_size_t),
                                           ctypes.POINTER(ctypes.c_long), ctypes.POINTER(ctypes.c_long)]
     c.mvx_copy.argtypes = [vp, vp, sz]

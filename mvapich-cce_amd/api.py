@@ -14,6 +14,7 @@ __all__ = [
     "MPI_Allreduce", "MPI_Reduce", "MPI_Reduce_scatter", "MPI_Scan", "MPI_Op_create", "MPI_Op_free", "op_create_device",
     "MPIR_call", "op_errno", "last_kernel", "last_kernel_symbol", "last_launch", "set_launch",
     "set_fortran_logical", "comm_reap", "host_register_enable", "host_unregister", "host_register_stats",
+    "host_hooks_active", "host_invalidate",
     "MPI_Type_contiguous", "MPI_Type_commit", "MPI_Type_free", "MPI_Type_extent", "MPI_Type_size",
     "MPI_Type_vector", "MPI_Type_hvector", "MPI_Type_indexed", "MPI_Type_hindexed", "MPI_Type_struct",
     "MPI_Type_lb", "MPI_Type_ub", "type_layout", "type_set_handle", "type_pack", "type_unpack",
@@ -483,8 +484,28 @@ def comm_reap():
 
 
 def host_register_enable(on=True, max_bytes=0):
-    """The pageable-buffer registration cache (mvx_host_register_enable)."""
-    return coll().mvx_host_register_enable(1 if on else 0, max_bytes)
+    """The pageable-buffer registration cache (mvx_host_register_enable).
+
+    A Python process loads libmvx.so with dlopen, so its release hooks are
+    not the process's (mvx_host_hooks_active() is 0 here): the cache runs in
+    mode 2, and the caller reports every release of a buffer it passed with
+    host_unregister / host_invalidate before the memory is freed.  A C
+    program linked with -lmvx gets mode 1, releases seen by the hooks."""
+    mode = 0
+    if on:
+        mode = 1 if coll().mvx_host_hooks_active() else 2
+    return coll().mvx_host_register_enable(mode, max_bytes)
+
+
+def host_hooks_active():
+    """mvx_host_hooks_active: libmvx.so's release hooks are the process's."""
+    return bool(coll().mvx_host_hooks_active())
+
+
+def host_invalidate(address, nbytes):
+    """mvx_host_invalidate: drop registrations overlapping [address,
+    address + nbytes), about to be released; returns how many."""
+    return coll().mvx_host_invalidate(address, nbytes)
 
 
 def host_unregister(buf):

@@ -58,7 +58,20 @@ static int plan_moves(const mvx_plan *P)
     return 0;
 }
 
+static int run_on(mvx_comm_t *c, const call_t *k, hipStream_t st, int blocking);
+
+/* every call runs on its communicator's device; the caller's stays current */
 static int run(mvx_comm_t *c, const call_t *k, hipStream_t st, int blocking)
+{
+    const int prev = mvxi_dev_enter(c->device);
+    int rc;
+    if (prev == MVXI_DEV_FAILED) return MPI_ERR_OTHER;
+    rc = run_on(c, k, st, blocking);
+    mvxi_dev_leave(c->device, prev);
+    return rc;
+}
+
+static int run_on(mvx_comm_t *c, const call_t *k, hipStream_t st, int blocking)
 {
     mvx_work *w = mvxi_work(c);
     mvx_plan *Pp;
@@ -301,10 +314,28 @@ int mvx_reduce_scatter_async(const void *sendbuf, void *recvbuf, const int *recv
  * staged pipeline and the call returns when they are written.  The plan,
  * transport and slice tables are the communicator's: one call at a time per
  * communicator (MPI-1.2 is not thread-safe either, coll.h:61-68). */
+static int run_multi_on(mvx_comm_t *c, int coll, void *const *sendbufs,
+                        void *const *recvbufs, long count, const int *recvcnts,
+                        MPI_Datatype dt, MPI_Op op, int root, int *rcs,
+                        hipStream_t st);
+
 static int run_multi(mvx_comm_t *c, int coll, void *const *sendbufs,
                      void *const *recvbufs, long count, const int *recvcnts,
                      MPI_Datatype dt, MPI_Op op, int root, int *rcs,
                      hipStream_t st)
+{
+    const int prev = mvxi_dev_enter(c->device);
+    int rc;
+    if (prev == MVXI_DEV_FAILED) return MPI_ERR_OTHER;
+    rc = run_multi_on(c, coll, sendbufs, recvbufs, count, recvcnts, dt, op, root, rcs, st);
+    mvxi_dev_leave(c->device, prev);
+    return rc;
+}
+
+static int run_multi_on(mvx_comm_t *c, int coll, void *const *sendbufs,
+                        void *const *recvbufs, long count, const int *recvcnts,
+                        MPI_Datatype dt, MPI_Op op, int root, int *rcs,
+                        hipStream_t st)
 {
     mvx_work *w = mvxi_work(c);
     mvx_plan *plans;

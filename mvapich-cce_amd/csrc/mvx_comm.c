@@ -184,15 +184,43 @@ int mvx_get_unique_id(void *id_out)
     return MPI_SUCCESS;
 }
 
-int mvx_comm_init(MPI_Comm *comm, int rank, int size, int device,
-                  const void *unique_id)
+/* ---- the caller's current device -----------------------------------------
+ * Communicator creation and every call that works on a communicator switch
+ * to its device for their duration and switch back: a C application driving
+ * two devices from one thread keeps the device it had selected. */
+int mvxi_dev_enter(int device)
+{
+    int prev = -1;
+    if (hipGetDevice(&prev) != hipSuccess) { (void)hipGetLastError(); prev = -1; }
+    if (prev != device && hipSetDevice(device) != hipSuccess) {
+        (void)hipGetLastError();
+        return MVXI_DEV_FAILED;
+    }
+    return prev;
+}
+
+void mvxi_dev_leave(int device, int prev)
+{
+    if (prev >= 0 && prev != device) (void)hipSetDevice(prev);
+}
+
+/* 0 if `device` can be selected and holds a context (a communicator can be
+ * created on it); MPI_ERR_OTHER otherwise.  The current device is kept. */
+int mvx_device_check(int device)
+{
+    int n = mvx_device_count(), prev, rc = MPI_SUCCESS;
+    if (device < 0 || device >= n) return MPI_ERR_OTHER;
+    prev = mvxi_dev_enter(device);
+    if (prev == MVXI_DEV_FAILED) return MPI_ERR_OTHER;
+    if (hipFree(NULL) != hipSuccess) { (void)hipGetLastError(); rc = MPI_ERR_OTHER; }
+    mvxi_dev_leave(device, prev);
+    return rc;
+}
+
+static int comm_init_rccl(MPI_Comm *comm, int rank, int size, int device, const void *unique_id)
 {
     ncclUniqueId id;
-    mvx_comm_t *c;
-    if (!comm || size < 1 || size > MVX_MAXP || rank < 0 || rank >= size)
-        return MPI_ERR_ARG;
-    if (hipSetDevice(device) != hipSuccess) return MPI_ERR_OTHER;
-    c = new_comm(comm);
+    mvx_comm_t *c = new_comm(comm);
     if (!c) return MPI_ERR_INTERN;
     c->rank = rank; c->size = size; c->device = device; c->local = 0;
     if (comm_flavour(c)) { c->used = 0; return MPI_ERR_OTHER; }
@@ -206,11 +234,25 @@ int mvx_comm_init(MPI_Comm *comm, int rank, int size, int device,
     return MPI_SUCCESS;
 }
 
+int mvx_comm_init(MPI_Comm *comm, int rank, int size, int device,
+                  const void *unique_id)
+{
+    int prev, rc;
+    if (!comm || size < 1 || size > MVX_MAXP || rank < 0 || rank >= size)
+        return MPI_ERR_ARG;
+    if ((prev = mvxi_dev_enter(device)) == MVXI_DEV_FAILED) return MPI_ERR_OTHER;
+    rc = comm_init_rccl(comm, rank, size, device, unique_id);
+    mvxi_dev_leave(device, prev);
+    return rc;
+}
+
 int mvx_comm_init_local(MPI_Comm *comm, int size, int device)
 {
     mvx_comm_t *c;
+    int prev;
     if (!comm || size < 1 || size > MVX_MAXP) return MPI_ERR_ARG;
-    if (hipSetDevice(device) != hipSuccess) return MPI_ERR_OTHER;
+    if ((prev = mvxi_dev_enter(device)) == MVXI_DEV_FAILED) return MPI_ERR_OTHER;
+    mvxi_dev_leave(device, prev);
     c = new_comm(comm);
     if (!c) return MPI_ERR_INTERN;
     c->rank = 0; c->size = size; c->device = device; c->local = 1;
@@ -227,6 +269,7 @@ int mvx_comm_init_transport_ex(MPI_Comm *comm, int rank, int size, int device,
 {
     mvx_comm_t *c;
     mvx_transport t;
+    int prev;
     if (!comm || !transport || bytes < MVX_TRANSPORT_BASE_BYTES || size < 1 || size > MVX_MAXP ||
         rank < 0 || rank >= size)
         return MPI_ERR_ARG;
@@ -234,7 +277,8 @@ int mvx_comm_init_transport_ex(MPI_Comm *comm, int rank, int size, int device,
     memcpy(&t, transport, bytes < sizeof t ? bytes : sizeof t);
     if (!t.start || !t.send || !t.recv || !t.end) return MPI_ERR_ARG;
     if (!t.alltoall || !t.allgather) t.alltoall = NULL, t.allgather = NULL;
-    if (hipSetDevice(device) != hipSuccess) return MPI_ERR_OTHER;
+    if ((prev = mvxi_dev_enter(device)) == MVXI_DEV_FAILED) return MPI_ERR_OTHER;
+    mvxi_dev_leave(device, prev);
     c = new_comm(comm);
     if (!c) return MPI_ERR_INTERN;
     c->rank = rank; c->size = size; c->device = device; c->local = 0;
@@ -365,8 +409,10 @@ static int park(mvx_comm_t *c)
 static int comm_release(MPI_Comm *comm, int abort)
 {
     mvx_comm_t *c = comm ? mvxi_get_comm(*comm) : NULL;
-    int i;
+    int i, device, prev;
     if (!c) return ERR_COMM_NULL_CODE;
+    device = c->device;
+    prev = mvxi_dev_enter(device);
     /* the graphs first: a captured RCCL group holds a reference on its
      * communicator, and ncclCommDestroy waits for every such reference to go
      * (measured: destroying the communicator first never returned).  An
@@ -405,6 +451,7 @@ static int comm_release(MPI_Comm *comm, int abort)
     if (c->handle == MPI_COMM_WORLD) g_have_world = 0;
     memset(c, 0, sizeof *c);
     *comm = 0;
+    mvxi_dev_leave(device, prev);
     return MPI_SUCCESS;
 }
 
@@ -518,6 +565,7 @@ int mvx_comm_rccl_native(MPI_Comm comm, int coll, const void *sendbuf, void *rec
     mvx_comm_t *c = mvxi_get_comm(comm);
     ncclDataType_t t;
     ncclResult_t r;
+    int prev;
     if (!c) return ERR_COMM_NULL_CODE;
     if (c->local || c->has_ops || !c->nccl) return MPI_ERR_COMM;
     if (dt == MPI_FLOAT) t = ncclFloat32;
@@ -526,9 +574,11 @@ int mvx_comm_rccl_native(MPI_Comm comm, int coll, const void *sendbuf, void *rec
     else if (dt == MPI_LONG || dt == MPI_LONG_LONG_INT) t = ncclInt64;
     else return MPI_ERR_TYPE;
     c->last_st = st;
+    if (coll != MVX_COLL_ALLREDUCE && coll != MVX_COLL_REDUCE_SCATTER) return MPI_ERR_ARG;
+    if ((prev = mvxi_dev_enter(c->device)) == MVXI_DEV_FAILED) return MPI_ERR_OTHER;
     if (coll == MVX_COLL_ALLREDUCE) r = ncclAllReduce(sendbuf, recvbuf, count, t, ncclSum, c->nccl, st);
-    else if (coll == MVX_COLL_REDUCE_SCATTER) r = ncclReduceScatter(sendbuf, recvbuf, count, t, ncclSum, c->nccl, st);
-    else return MPI_ERR_ARG;
+    else r = ncclReduceScatter(sendbuf, recvbuf, count, t, ncclSum, c->nccl, st);
+    mvxi_dev_leave(c->device, prev);
     return r == ncclSuccess ? MPI_SUCCESS : MPI_ERR_OTHER;
 }
 
@@ -558,9 +608,12 @@ int mvx_comm_set_phase_timing(MPI_Comm comm, int on)
     int i;
     if (!c) return ERR_COMM_NULL_CODE;
     if (on && !c->tev_ready) {
-        if (hipSetDevice(c->device) != hipSuccess) return MPI_ERR_OTHER;
-        for (i = 0; i < 4; i++)
-            if (hipEventCreate(&c->tev[i]) != hipSuccess) return MPI_ERR_OTHER;
+        const int prev = mvxi_dev_enter(c->device);
+        int rc = prev == MVXI_DEV_FAILED ? MPI_ERR_OTHER : MPI_SUCCESS;
+        for (i = 0; i < 4 && !rc; i++)
+            if (hipEventCreate(&c->tev[i]) != hipSuccess) rc = MPI_ERR_OTHER;
+        if (prev != MVXI_DEV_FAILED) mvxi_dev_leave(c->device, prev);
+        if (rc) return rc;
         c->tev_ready = 1;
     }
     c->timing = on ? 1 : 0;
@@ -627,7 +680,11 @@ int mvxi_grow_host(char **buf, size_t *have, size_t need)
 int mvx_comm_reserve(MPI_Comm comm, size_t bytes)
 {
     mvx_comm_t *c = mvxi_get_comm(comm);
+    int prev, rc;
     if (!c) return ERR_COMM_NULL_CODE;
     mvx_comm_reap();
-    return mvxi_grow(&c->pool, &c->pool_bytes, bytes);
+    if ((prev = mvxi_dev_enter(c->device)) == MVXI_DEV_FAILED) return MPI_ERR_OTHER;
+    rc = mvxi_grow(&c->pool, &c->pool_bytes, bytes);
+    mvxi_dev_leave(c->device, prev);
+    return rc;
 }

@@ -318,7 +318,29 @@ static void pipe_slice(const job_t *J, int r, long t, long cs, char *region_base
     if (Q->c_dst_tmp) X->tmp_off = (size_t)(tmp + t * cs * Q->esize - region_base);
 }
 
+static int graph_streams(mvx_comm_t *c);
+static int run_device_pipe_on(mvx_comm_t *c, const job_t *J, hipStream_t st);
+
+/* The combine stream may be a blocking stream (hipExtStreamCreateWithCUMask
+ * takes no flags), and the legacy null stream waits for every blocking
+ * stream: slice t + 1's transfers issued on it would wait for slice t's
+ * combine.  A null-stream call therefore runs its slices on the
+ * communicator's non-blocking stream, forked from the null stream and joined
+ * back (as a null-stream graph launch does); a capture is already on it. */
 static int run_device_pipe(mvx_comm_t *c, const job_t *J, hipStream_t st)
+{
+    int rc;
+    if (st || mvxi_capturing) return run_device_pipe_on(c, J, st);
+    if ((rc = graph_streams(c))) return rc;
+    if (hipEventRecord(c->gev[0], st) != hipSuccess || hipStreamWaitEvent(c->gstream, c->gev[0], 0) != hipSuccess)
+        return MPI_ERR_OTHER;
+    rc = run_device_pipe_on(c, J, c->gstream);
+    if (hipEventRecord(c->gev[1], c->gstream) != hipSuccess || hipStreamWaitEvent(st, c->gev[1], 0) != hipSuccess)
+        return rc ? rc : MPI_ERR_OTHER;
+    return rc;
+}
+
+static int run_device_pipe_on(mvx_comm_t *c, const job_t *J, hipStream_t st)
 {
     mvx_work *w = mvxi_work(c);
     rank_exec_t *X0, (*X)[MVX_MAXP];
@@ -342,6 +364,9 @@ static int run_device_pipe(mvx_comm_t *c, const job_t *J, hipStream_t st)
     c->ran_exch = MVX_EXCH_PIPE;
     for (r = 0; r < J->nr; r++) {
         mvxi_plan_slice(&J->P[r], 0, cs, &pl[0][r]);
+        /* a non-root Reduce's result goes to the shared unsliced temporary
+         * (pipe_slice): no slot for it in the per-slice regions */
+        pl[0][r].c_dst_tmp = 0;
         X0[r].sendbuf = J->send[r];
         X0[r].recvbuf = J->recv[r];
     }

@@ -18,18 +18,22 @@
  * kept, so later calls on it DMA directly instead of copying through the
  * bounce slots.  Entries are page-aligned [base, end) ranges, evicted least
  * recently used past MVX_HOST_REGISTER_MAX_MIB (default 16384); ranges under
- * MVX_HOST_REGISTER_MIN_KIB (default 1024) are never registered.  The
- * reference learns of freed memory through malloc hooks (mem_hooks.c); here
- * the contract is mvx_host_unregister(addr) before the memory is freed.
- * The contract is not optional: on MI355X a registered range that is freed
- * (unmapped) and handed out again by malloc at the same address, with no
- * mvx_host_unregister in between, left the GPU in the memory-access-fault
- * state at its next DMA (round 4).  No CPU-side check
- * sees the free, and a probing DMA would fault the same way; that is why
- * the cache is off unless the application asks for it and keeps the
- * contract.
+ * MVX_HOST_REGISTER_MIN_KIB (default 1024) are never registered.
+ * A registration must not outlive its memory: on MI355X a registered range
+ * that was freed (unmapped) and handed out again by malloc at the same
+ * address left the GPU in the memory-access-fault state at its next DMA
+ * (round 4), and no CPU-side check can see the free
+ * afterwards.  So, as the reference learns of released memory through its
+ * hooks (mem_hooks.c), libmvx.so interposes the calls that release memory
+ * (free, realloc, munmap, mremap, madvise, sbrk; below) and drops every
+ * registration inside a released range first.  Mode 1 of the cache needs
+ * those hooks in effect; mode 2 is for callers that report releases
+ * themselves (mvx_host_unregister / mvx_host_invalidate: a dlopen'ed
+ * library, or a host MPI whose own hooks call mvx_host_invalidate).
  */
+#define _GNU_SOURCE 1   /* RTLD_NEXT, MREMAP_FIXED, malloc_usable_size */
 #include <pthread.h>
+#include <stdarg.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -176,19 +180,29 @@ int mvx_copy_threads(void)
     return n;
 }
 
-/* ---- the registration cache ------------------------------------------------ */
+/* ---- the registration cache ------------------------------------------------
+ * Entries are page-aligned [base, end) ranges.  No HIP call is made while
+ * the table's mutex is held: entries leave the table under the lock and are
+ * unregistered after it is released (the release hooks below run inside
+ * free(), which HIP's own threads call too, so they must never wait for a
+ * thread that is inside HIP). */
 
 #define REG_MAX 64
 #define PAGE 4096UL
 typedef struct { uintptr_t base, end; unsigned long stamp; } reg_t;
 static struct {
     pthread_mutex_t mu;
-    int init, on;
+    int init, on, dry;
     size_t min_bytes, max_bytes, total;
-    unsigned long clock, hits, misses, evictions, failures;
+    unsigned long clock, hits, misses, evictions, failures, invalidations;
     int n;
     reg_t e[REG_MAX];
-} g_reg = { PTHREAD_MUTEX_INITIALIZER, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, {{0, 0, 0}} };
+} g_reg = { PTHREAD_MUTEX_INITIALIZER, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, {{0, 0, 0}} };
+
+/* read without the lock by the release hooks: entries exist, and the span
+ * [lo, hi) covering all of them (a superset while entries change) */
+static volatile int g_reg_live;
+static volatile uintptr_t g_reg_lo, g_reg_hi;
 
 static void reg_env(void)
 {
@@ -196,46 +210,108 @@ static void reg_env(void)
     if (g_reg.init) return;
     g_reg.init = 1;
     v = getenv("MVX_HOST_REGISTER");
-    g_reg.on = v && atoi(v) == 1;
+    g_reg.on = v ? atoi(v) : 0;
+    if (g_reg.on == 1 && !mvx_host_hooks_active()) g_reg.on = 0;   /* nothing would see a release */
+    if (g_reg.on != 1 && g_reg.on != 2) g_reg.on = 0;
+    v = getenv("MVX_HOST_REGISTER_DRY");        /* tests: track ranges, no page-locking */
+    g_reg.dry = v && atoi(v) == 1;
     v = getenv("MVX_HOST_REGISTER_MIN_KIB");
     g_reg.min_bytes = (size_t)(v ? atol(v) : 1024) << 10;
     v = getenv("MVX_HOST_REGISTER_MAX_MIB");
     g_reg.max_bytes = (size_t)(v ? atol(v) : 16384) << 20;
 }
 
-static void reg_drop(int i)
+static void reg_span_locked(void)
 {
-    (void)hipHostUnregister((void *)g_reg.e[i].base);
-    (void)hipGetLastError();
+    uintptr_t lo = UINTPTR_MAX, hi = 0;
+    int i;
+    for (i = 0; i < g_reg.n; i++) {
+        if (g_reg.e[i].base < lo) lo = g_reg.e[i].base;
+        if (g_reg.e[i].end > hi) hi = g_reg.e[i].end;
+    }
+    __atomic_store_n(&g_reg_lo, g_reg.n ? lo : UINTPTR_MAX, __ATOMIC_RELAXED);
+    __atomic_store_n(&g_reg_hi, g_reg.n ? hi : 0, __ATOMIC_RELAXED);
+    __atomic_store_n(&g_reg_live, g_reg.n, __ATOMIC_RELEASE);
+}
+
+/* entries leaving the table, unregistered once the lock is dropped */
+typedef struct { int n; reg_t e[REG_MAX]; } reg_out_t;
+
+static void reg_take_locked(int i, reg_out_t *out)
+{
+    out->e[out->n++] = g_reg.e[i];
     g_reg.total -= g_reg.e[i].end - g_reg.e[i].base;
     g_reg.e[i] = g_reg.e[--g_reg.n];
 }
 
-static void reg_drop_all(void)
+static void reg_release(const reg_out_t *out, int dry)
 {
-    while (g_reg.n) reg_drop(g_reg.n - 1);
+    int i;
+    if (dry) return;
+    for (i = 0; i < out->n; i++) {
+        (void)hipHostUnregister((void *)out->e[i].base);
+        (void)hipGetLastError();
+    }
+}
+
+/* every entry overlapping [lo, hi) leaves the table and is unregistered */
+static int reg_invalidate(uintptr_t lo, uintptr_t hi)
+{
+    reg_out_t out;
+    int i, dry;
+    out.n = 0;
+    pthread_mutex_lock(&g_reg.mu);
+    for (i = g_reg.n - 1; i >= 0; i--)
+        if (g_reg.e[i].base < hi && lo < g_reg.e[i].end) reg_take_locked(i, &out);
+    g_reg.invalidations += (unsigned long)out.n;
+    reg_span_locked();
+    dry = g_reg.dry;
+    pthread_mutex_unlock(&g_reg.mu);
+    reg_release(&out, dry);
+    return out.n;
+}
+
+int mvx_host_invalidate(const void *addr, size_t bytes)
+{
+    const uintptr_t a = (uintptr_t)addr;
+    if (!bytes || !__atomic_load_n(&g_reg_live, __ATOMIC_ACQUIRE)) return 0;
+    return reg_invalidate(a & ~(PAGE - 1), a + bytes);
 }
 
 int mvx_host_register_enable(int on, size_t max_bytes)
 {
+    reg_out_t out;
+    int dry;
+    if (on < 0 || on > 2) return MPI_ERR_ARG;
+    if (on == 1 && !mvx_host_hooks_active()) return MPI_ERR_OTHER;
+    out.n = 0;
     pthread_mutex_lock(&g_reg.mu);
     reg_env();
-    g_reg.on = on ? 1 : 0;
+    g_reg.on = on;
     if (max_bytes) g_reg.max_bytes = max_bytes;
-    if (!g_reg.on) reg_drop_all();
+    if (!g_reg.on)
+        while (g_reg.n) reg_take_locked(g_reg.n - 1, &out);
+    reg_span_locked();
+    dry = g_reg.dry;
     pthread_mutex_unlock(&g_reg.mu);
+    reg_release(&out, dry);
     return 0;
 }
 
 int mvx_host_unregister(const void *addr)
 {
     const uintptr_t a = (uintptr_t)addr;
-    int i, found = 0;
+    reg_out_t out;
+    int i, dry;
+    out.n = 0;
     pthread_mutex_lock(&g_reg.mu);
     for (i = g_reg.n - 1; i >= 0; i--)
-        if (g_reg.e[i].base <= a && a < g_reg.e[i].end) { reg_drop(i); found = 1; }
+        if (g_reg.e[i].base <= a && a < g_reg.e[i].end) reg_take_locked(i, &out);
+    reg_span_locked();
+    dry = g_reg.dry;
     pthread_mutex_unlock(&g_reg.mu);
-    return found ? 0 : MPI_ERR_ARG;
+    reg_release(&out, dry);
+    return out.n ? 0 : MPI_ERR_ARG;
 }
 
 int mvx_host_register_stats(long *entries, size_t *bytes, long *hits, long *misses)
@@ -250,12 +326,23 @@ int mvx_host_register_stats(long *entries, size_t *bytes, long *hits, long *miss
     return 0;
 }
 
-int mvxi_buf_kind_range(const void *p, size_t bytes)
+long mvx_host_register_invalidations(void)
 {
-    const int k = mvx_buf_kind(p);
+    long n;
+    pthread_mutex_lock(&g_reg.mu);
+    n = (long)g_reg.invalidations;
+    pthread_mutex_unlock(&g_reg.mu);
+    return n;
+}
+
+/* Register [p, p + bytes) (page-widened) in the cache; MVX_BUF_PINNED when
+ * the range is (now) registered, else what mvx_buf_kind says.  `k` is p's
+ * kind as mvx_buf_kind reported it. */
+static int reg_range(const void *p, size_t bytes, int k)
+{
     uintptr_t base, end;
-    int i, cover = -1, overlap = 0;
-    if (k == MVX_BUF_DEVICE || !p || !bytes) return k;
+    reg_out_t out;
+    int i, cover = -1, overlap = 0, dry, ok;
     pthread_mutex_lock(&g_reg.mu);
     reg_env();
     if (!g_reg.on && !g_reg.n) { pthread_mutex_unlock(&g_reg.mu); return k; }
@@ -277,28 +364,38 @@ int mvxi_buf_kind_range(const void *p, size_t bytes)
     }
     /* a range that runs past a registration of ours: the union replaces it
      * (a DMA must never read past the pinned pages) */
+    out.n = 0;
     for (i = g_reg.n - 1; i >= 0; i--)
         if (g_reg.e[i].base < end && base < g_reg.e[i].end) {
             if (g_reg.e[i].base < base) base = g_reg.e[i].base;
             if (g_reg.e[i].end > end) end = g_reg.e[i].end;
-            reg_drop(i);
+            reg_take_locked(i, &out);
         }
-    if (!g_reg.on || end - base < g_reg.min_bytes || end - base > g_reg.max_bytes) {
-        pthread_mutex_unlock(&g_reg.mu);
-        return mvx_buf_kind(p);
-    }
-    while (g_reg.n && (g_reg.n == REG_MAX || g_reg.total + (end - base) > g_reg.max_bytes)) {
+    ok = g_reg.on && end - base >= g_reg.min_bytes && end - base <= g_reg.max_bytes;
+    while (ok && g_reg.n && (g_reg.n == REG_MAX || g_reg.total + (end - base) > g_reg.max_bytes)) {
         int lru = 0;                                    /* evict the least recently used */
         for (i = 1; i < g_reg.n; i++)
             if (g_reg.e[i].stamp < g_reg.e[lru].stamp) lru = i;
-        reg_drop(lru);
+        reg_take_locked(lru, &out);
         g_reg.evictions++;
     }
-    g_reg.misses++;
-    if (hipHostRegister((void *)base, end - base, hipHostRegisterDefault) != hipSuccess) {   /* dreg_register */
+    if (ok) g_reg.misses++;
+    reg_span_locked();
+    dry = g_reg.dry;
+    pthread_mutex_unlock(&g_reg.mu);
+    reg_release(&out, dry);
+    if (!ok) return mvx_buf_kind(p);
+    if (!dry && hipHostRegister((void *)base, end - base, hipHostRegisterDefault) != hipSuccess) {   /* dreg_register */
         (void)hipGetLastError();
+        pthread_mutex_lock(&g_reg.mu);
         g_reg.failures++;
         pthread_mutex_unlock(&g_reg.mu);
+        return mvx_buf_kind(p);
+    }
+    pthread_mutex_lock(&g_reg.mu);
+    if (g_reg.n == REG_MAX) {                           /* filled meanwhile: keep it out */
+        pthread_mutex_unlock(&g_reg.mu);
+        if (!dry) (void)hipHostUnregister((void *)base);
         return mvx_buf_kind(p);
     }
     g_reg.e[g_reg.n].base = base;
@@ -306,9 +403,154 @@ int mvxi_buf_kind_range(const void *p, size_t bytes)
     g_reg.e[g_reg.n].stamp = ++g_reg.clock;
     g_reg.n++;
     g_reg.total += end - base;
+    reg_span_locked();
     pthread_mutex_unlock(&g_reg.mu);
     return MVX_BUF_PINNED;
 }
+
+int mvxi_buf_kind_range(const void *p, size_t bytes)
+{
+    const int k = mvx_buf_kind(p);
+    if (k == MVX_BUF_DEVICE || !p || !bytes) return k;
+    return reg_range(p, bytes, k);
+}
+
+/* explicit registration (dreg_register without a transfer) */
+int mvx_host_register(const void *addr, size_t bytes)
+{
+    int on;
+    if (!addr || !bytes) return MPI_ERR_ARG;
+    pthread_mutex_lock(&g_reg.mu);
+    reg_env();
+    on = g_reg.on;
+    pthread_mutex_unlock(&g_reg.mu);
+    if (!on) return MPI_ERR_OTHER;
+    return reg_range(addr, bytes, g_reg.dry ? MVX_BUF_PAGEABLE : mvx_buf_kind(addr)) == MVX_BUF_PINNED
+               ? MPI_SUCCESS : MPI_ERR_OTHER;
+}
+
+/* ---- release hooks (mpid/ch_gen2/mem_hooks.c:97-132) ------------------------
+ * MVAPICH interposes munmap and its own malloc's negative sbrk and drops
+ * every registration inside a released range before the release
+ * (find_and_free_dregs_inside, dreg.c:1063).  With glibc's malloc the
+ * releases happen inside free() / realloc() (which unmap or trim through
+ * libc-internal calls no munmap interposer sees), so libmvx.so interposes
+ * those too: free / realloc drop registrations overlapping the block
+ * [p, p + malloc_usable_size(p)), munmap / mremap / madvise (DONTNEED, FREE,
+ * REMOVE) / negative sbrk the range they release.  Then the real call runs
+ * (the next definition in the lookup order: glibc's, or an allocator
+ * interposed after this library).  The hooks take effect when libmvx.so is
+ * in the program's global scope ahead of libc -- a program linked with
+ * -lmvx (mvx_host_hooks_active reports it); a library dlopen'ed without
+ * that (ctypes) runs the cache under the unregister contract instead.
+ * libmvx_embed.so has no hooks: the host MPI's own (mem_hooks.c) call
+ * mvx_host_invalidate. */
+#ifndef MVX_NO_MEMHOOKS
+#include <dlfcn.h>
+#include <malloc.h>
+#include <sys/mman.h>
+#include <sys/syscall.h>
+
+extern void __libc_free(void *);
+extern void *__libc_realloc(void *, size_t);
+
+static void (*real_free)(void *);
+static void *(*real_realloc)(void *, size_t);
+static int (*real_munmap)(void *, size_t);
+static void *(*real_mremap)(void *, size_t, size_t, int, ...);
+static int (*real_madvise)(void *, size_t, int);
+static void *(*real_sbrk)(intptr_t);
+
+__attribute__((constructor)) static void hooks_resolve(void)
+{
+    real_free = (void (*)(void *))dlsym(RTLD_NEXT, "free");
+    real_realloc = (void *(*)(void *, size_t))dlsym(RTLD_NEXT, "realloc");
+    real_munmap = (int (*)(void *, size_t))dlsym(RTLD_NEXT, "munmap");
+    real_mremap = (void *(*)(void *, size_t, size_t, int, ...))dlsym(RTLD_NEXT, "mremap");
+    real_madvise = (int (*)(void *, size_t, int))dlsym(RTLD_NEXT, "madvise");
+    real_sbrk = (void *(*)(intptr_t))dlsym(RTLD_NEXT, "sbrk");
+}
+
+/* cheap test first: no entries, or [lo, hi) outside every entry's span */
+static void hook_release(uintptr_t lo, uintptr_t hi)
+{
+    if (!__atomic_load_n(&g_reg_live, __ATOMIC_ACQUIRE) || hi <= lo) return;
+    if (hi <= __atomic_load_n(&g_reg_lo, __ATOMIC_RELAXED) || lo >= __atomic_load_n(&g_reg_hi, __ATOMIC_RELAXED))
+        return;
+    reg_invalidate(lo & ~(PAGE - 1), hi);
+}
+
+static void hook_block(void *p)
+{
+    if (p && __atomic_load_n(&g_reg_live, __ATOMIC_ACQUIRE))
+        hook_release((uintptr_t)p, (uintptr_t)p + malloc_usable_size(p));
+}
+
+/* the definitions, named so their own addresses can be compared with what
+ * the program's lookup finds (a reference to `free` here would go through
+ * the PLT to whichever free is the process's) */
+static void hook_free(void *p)
+{
+    hook_block(p);
+    if (real_free) real_free(p);
+    else __libc_free(p);
+}
+void free(void *p) __attribute__((alias("hook_free")));
+
+void *realloc(void *p, size_t n)
+{
+    hook_block(p);
+    return real_realloc ? real_realloc(p, n) : __libc_realloc(p, n);
+}
+
+static int hook_munmap(void *addr, size_t len)
+{
+    hook_release((uintptr_t)addr, (uintptr_t)addr + len);
+    if (real_munmap) return real_munmap(addr, len);
+    return (int)syscall(SYS_munmap, addr, len);
+}
+int munmap(void *addr, size_t len) __attribute__((alias("hook_munmap")));
+
+void *mremap(void *old, size_t old_len, size_t new_len, int flags, ...)
+{
+    void *target = NULL;
+    va_list ap;
+    hook_release((uintptr_t)old, (uintptr_t)old + old_len);
+    if (flags & MREMAP_FIXED) {
+        va_start(ap, flags);
+        target = va_arg(ap, void *);
+        va_end(ap);
+        hook_release((uintptr_t)target, (uintptr_t)target + new_len);   /* replaced by the move */
+    }
+    if (real_mremap) return real_mremap(old, old_len, new_len, flags, target);
+    return (void *)syscall(SYS_mremap, old, old_len, new_len, flags, target);
+}
+
+int madvise(void *addr, size_t len, int advice)
+{
+    if (advice == MADV_DONTNEED || advice == MADV_FREE || advice == MADV_REMOVE)
+        hook_release((uintptr_t)addr, (uintptr_t)addr + len);
+    if (real_madvise) return real_madvise(addr, len, advice);
+    return (int)syscall(SYS_madvise, addr, len, advice);
+}
+
+void *sbrk(intptr_t delta)
+{
+    extern void *__sbrk(intptr_t);
+    if (delta < 0) {                                   /* mvapich_sbrk */
+        const uintptr_t cur = (uintptr_t)(real_sbrk ? real_sbrk(0) : __sbrk(0));
+        hook_release(cur + (uintptr_t)delta, cur);
+    }
+    return real_sbrk ? real_sbrk(delta) : __sbrk(delta);
+}
+
+int mvx_host_hooks_active(void)
+{
+    return dlsym(RTLD_DEFAULT, "free") == (void *)hook_free && dlsym(RTLD_DEFAULT, "munmap") == (void *)hook_munmap;
+}
+#else
+int mvx_host_hooks_active(void) { return 0; }
+#endif
 
 
 /* A stream for work that must run beside the caller's stream.  HIP spreads

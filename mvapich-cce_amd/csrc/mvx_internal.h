@@ -139,6 +139,8 @@ MVXI size_t mvxi_region_layout(mvx_comm_t *c, rank_exec_t *X, const job_t *J, co
 MVXI int mvxi_job_layout(mvx_comm_t *c, rank_exec_t *X, const job_t *J, const mvx_plan *Q);
 MVXI void mvxi_plan_slice(const mvx_plan *P, long i, long cs, mvx_plan *Q);
 MVXI long mvxi_plan_span(const mvx_plan *P);
+/* the slice schedule's slice length for a call's plan, 0 = unsliced (mvx_stage.c) */
+MVXI long mvxi_slice_elems(const mvx_plan *P);
 MVXI int mvxi_send_ranges(const mvx_plan *Q, mvx_range *v);
 MVXI int mvxi_recv_ranges(const mvx_plan *Q, mvx_range *v);
 
@@ -253,6 +255,11 @@ MVXI mvx_work *mvxi_work(mvx_comm_t *c);
 MVXI int mvxi_grow(char **buf, size_t *have, size_t need);
 MVXI int mvxi_grow_host(char **buf, size_t *have, size_t need);
 MVXI void mvxi_xport_comm(mvx_xport *t, mvx_comm_t *c, hipStream_t st);
+/* switch to `device` for a call and back: enter returns the caller's device
+ * (-1 unknown), or MVXI_DEV_FAILED when `device` cannot be selected */
+#define MVXI_DEV_FAILED (-2)
+MVXI int mvxi_dev_enter(int device);
+MVXI void mvxi_dev_leave(int device, int prev);
 
 /* per-phase timing: event i of a timed call (no-op when timing is off) */
 #define TEV_NONE 0

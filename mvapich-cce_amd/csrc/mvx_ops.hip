@@ -109,6 +109,7 @@ static const KSet *lookup(int op, int dtype, int *rc)
     case MPI_SUM: case MPI_PROD:
         return lookup_arith(op, ek);
     case MPI_LAND: case MPI_LOR: case MPI_LXOR: case MPI_BAND: case MPI_BOR: case MPI_BXOR:
+        if (ek == EK_LOGICAL && flog_sync()) { *rc = MPI_ERR_OTHER; return nullptr; }
         return lookup_logic(op, ek);
     case MPI_MAXLOC: case MPI_MINLOC:
         return lookup_loc(op, ek);

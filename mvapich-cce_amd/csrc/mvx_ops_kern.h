@@ -873,6 +873,7 @@ enum { EK_NONE = 0, EK_I8, EK_U8, EK_BYTE, EK_I16, EK_U16, EK_I32, EK_U32,
 const KSet *lookup_cmp(int op, int ek);     // MAX, MIN           mvx_ops_cmp.hip
 const KSet *lookup_arith(int op, int ek);   // SUM, PROD          mvx_ops_arith.hip
 const KSet *lookup_logic(int op, int ek);   // L* and B* ops      mvx_ops_logic.hip
+int flog_sync();                            // MPI_LOGICAL's words on this device (mvx_ops_logic.hip)
 const KSet *lookup_loc(int op, int ek);     // MAXLOC, MINLOC     mvx_ops_loc.hip
 
 }  // namespace mvx

@@ -5,9 +5,14 @@
  * host, so host operands are streamed through HBM and the device path runs
  * on them there:
  *
- *   HBM mirrors      one rank per process at p > 1 (default): the call moves
- *                    exactly what a device-buffer call moves, so ranks may
- *                    mix buffer kinds in one call, as MPI allows
+ *   slice schedule   one rank per process at p > 1, a blocking call of at
+ *                    least MVX_SLICE_MIN_MIB: every rank runs the call in the
+ *                    same slices whatever its buffers' kind, so a host-buffer
+ *                    rank overlaps H2D, the collective and D2H of successive
+ *                    slices and still pairs with device-buffer ranks
+ *   HBM mirrors      one rank per process at p > 1, smaller calls: the call
+ *                    moves exactly what a device-buffer call moves, so ranks
+ *                    may mix buffer kinds in one call, as MPI allows
  *   sliced pipeline  p = 1, virtual communicators, or every rank promising
  *                    host buffers (mvx_comm_set_host_pipeline): H2D, the
  *                    collective and D2H of successive slices overlap
@@ -16,6 +21,7 @@
  * All staging resources (streams, events, bounce slots, slice plans) are the
  * communicator's (mvx_work).
  */
+#include <stdlib.h>
 #include <string.h>
 
 #include "mvx_internal.h"
@@ -68,6 +74,7 @@ typedef struct {
     int spin[MVX_MAXP], rpin[MVX_MAXP];        /* ... and page-locked */
     long cs;                                   /* slice length, elements */
     int single;                                /* the job is one slice */
+    int any_host;                              /* some buffer is host memory */
 } stage_job_t;
 
 
@@ -81,6 +88,7 @@ static int stage_in(stage_job_t *S, const mvx_plan *Q, long i, hipStream_t st)
     mvx_range v[MVX_MAXP + 1];
     size_t boff = 0;
     int r, n, j;
+    if (!S->any_host) return MPI_SUCCESS;
     if (!S->single && i >= STAGE_NB && hipEventSynchronize(S->R->ein[b]) != hipSuccess) return MPI_ERR_OTHER;
     for (r = 0; r < S->J->nr; r++) {
         const long E = Q[r].esize;
@@ -113,6 +121,7 @@ static int stage_out(stage_job_t *S, const mvx_plan *Q, long i, hipStream_t st)
     mvx_range v[MVX_MAXP + 1];
     size_t boff = 0;
     int r, n, j;
+    if (!S->any_host) return MPI_SUCCESS;
     if (!S->single && (hipEventRecord(S->R->ex[b], st) != hipSuccess ||
                        hipStreamWaitEvent(S->R->sd, S->R->ex[b], 0) != hipSuccess))
         return MPI_ERR_OTHER;
@@ -139,6 +148,7 @@ static int stage_drain(stage_job_t *S, const mvx_plan *Q, long i, hipStream_t st
     mvx_range v[MVX_MAXP + 1];
     size_t boff = 0;
     int r, n, j;
+    if (!S->any_host) return MPI_SUCCESS;
     if ((S->single ? hipStreamSynchronize(st) : hipEventSynchronize(S->R->eout[b])) != hipSuccess)
         return MPI_ERR_OTHER;
     for (r = 0; r < S->J->nr; r++) {
@@ -154,7 +164,16 @@ static int stage_drain(stage_job_t *S, const mvx_plan *Q, long i, hipStream_t st
     return MPI_SUCCESS;
 }
 
+/* cs_fixed > 0: the slice length every rank of the call computed alike
+ * (slice_elems); 0: the pipeline's own, from this process's pieces */
+static int run_staged_cs(mvx_comm_t *c, const job_t *J, hipStream_t st, long cs_fixed);
+
 int mvxi_run_staged(mvx_comm_t *c, const job_t *J, hipStream_t st)
+{
+    return run_staged_cs(c, J, st, 0);
+}
+
+static int run_staged_cs(mvx_comm_t *c, const job_t *J, hipStream_t st, long cs_fixed)
 {
     mvx_work *w = mvxi_work(c);
     stage_job_t S;
@@ -175,6 +194,7 @@ int mvxi_run_staged(mvx_comm_t *c, const job_t *J, hipStream_t st)
         S.rhost[r] = J->rkind[r] != MVX_BUF_DEVICE;
         S.spin[r] = J->skind[r] == MVX_BUF_PINNED;
         S.rpin[r] = J->rkind[r] == MVX_BUF_PINNED;
+        S.any_host |= S.shost[r] || S.rhost[r];
         off[2 * r] = need;
         if (S.shost[r]) need = al256(need + (size_t)(J->nsend[r] * E));
         off[2 * r + 1] = need;
@@ -213,13 +233,14 @@ int mvxi_run_staged(mvx_comm_t *c, const job_t *J, hipStream_t st)
                             : STAGE_SLICE_BYTES / (E * J->P[0].p);
         cs -= cs % m;
         if (cs < m) cs = m;
+        if (cs_fixed > 0) cs = cs_fixed;
         S.cs = cs;
         bounce = (size_t)pieces * al256((size_t)(cs * E));
         if (bounce < 4096) bounce = 4096;
     }
     nsl = span > 0 ? (span + S.cs - 1) / S.cs : 0;
     S.single = nsl <= 1;
-    if ((rc = stage_init(S.R, bounce))) return rc;
+    if (S.any_host && (rc = stage_init(S.R, bounce))) return rc;
     for (r = 0; r < J->nr; r++) mvxi_plan_slice(&J->P[r], 0, S.cs, &w->slice[0][r]);
     if ((rc = mvxi_job_layout(c, X, J, w->slice[0]))) return rc;   /* slice 0 is the largest */
     for (i = 0; i < nsl; i++) {
@@ -478,10 +499,54 @@ int mvxi_typed_copy(mvx_comm_t *c, int dt, long n, const char *send, char *recv,
     return packed_finish(K, &T, B, st, sync || B->smir[0] || B->rmir[0]);
 }
 
+/* ---- the slice schedule: large calls at p > 1, any buffer kind ----------
+ * MPI lets every rank of a call pass device or host memory.  A host-buffer
+ * rank overlaps its PCIe copies with the collective only by running the
+ * collective in slices, and RCCL pairs a rank's transfers with its peers'
+ * only if they are the same messages -- so the slices cannot depend on the
+ * kinds.  A blocking call at p > 1 whose vector (count x size: the same on
+ * every rank) is at least MVX_SLICE_MIN_MIB (default 64) runs in slices on
+ * every rank, of MVX_SLICE_MIB (default 32) of the vector each, from
+ * quantities every rank holds alike (count, p, type size): slice i of every
+ * block is its elements [i cs, (i + 1) cs) (mvxi_plan_slice), run as phases
+ * A, B, C (P2P) on the call's stream.  A device-buffer rank issues its
+ * slices back to back; a host-buffer rank wraps each slice in its H2D (one
+ * stream) and D2H (another), so both PCIe directions and the collective
+ * overlap (run_staged_cs).  The bits are the unsliced plan's (every slice
+ * keeps every block boundary).  Stream-ordered calls (mvx_*_async, device
+ * buffers by contract) and smaller calls keep the unsliced schedule. */
+static long env_mib(const char *name, long dflt)
+{
+    const char *v = getenv(name);
+    return (v && atol(v) > 0 ? atol(v) : dflt) << 20;
+}
+
+/* elements per slice of every block, or 0: the call runs unsliced */
+long mvxi_slice_elems(const mvx_plan *P)
+{
+    const long E = P->esize, N = P->count, p = P->p;
+    const long vbytes = N * E, min = env_mib("MVX_SLICE_MIN_MIB", 64), per = env_mib("MVX_SLICE_MIB", 32);
+    long g = E, h = 256, m, nsl, blk, cs;
+    if (p < 2 || E <= 0 || N <= 0 || vbytes < min) return 0;
+    nsl = (vbytes + per - 1) / per;
+    if (nsl < 2) return 0;
+    while (h) { const long t = g % h; g = h; h = t; }      /* gcd(E, 256) */
+    m = 256 / g;                                            /* slices start 256-byte aligned */
+    blk = (N + p - 1) / p;
+    cs = (blk + nsl - 1) / nsl;
+    cs = (cs + m - 1) / m * m;
+    return cs;
+}
+
 int mvxi_run_job(mvx_comm_t *c, job_t *J, hipStream_t st, int blocking)
 {
     int rc;
+    long cs;
     if (J->P[0].packed) return mvxi_run_job_packed(c, J, st, blocking);
+    if (blocking && J->nr == 1 && !c->local && (cs = mvxi_slice_elems(&J->P[0])) > 0) {
+        mvxi_job_kinds(J);
+        return run_staged_cs(c, J, st, cs);
+    }
     if (mvxi_job_kinds(J)) {
         if (!blocking) return MPI_ERR_BUFFER;
         if (J->nr == 1 && J->P[0].p > 1 && !c->host_sliced) return run_mirrored(c, J, st);

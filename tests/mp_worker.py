@@ -7,7 +7,7 @@ the collectives through its libmvx.so communicator and compares its own
 result with the oracle's replay of the reference schedule
 (oracle/coll_sim.c) computed over all ranks' inputs.  Writes a JSON report.
 
-  mp_worker.py RANK WORLD PORT OUT.json TRANSPORT(host|rccl|rccl-net) SUITE(small|random|full|mixed|graph)
+  mp_worker.py RANK WORLD PORT OUT.json TRANSPORT(host|rccl|rccl-net) SUITE(small|random|full|mixed|sliced|graph)
 
 rccl-net: RCCL communicators whose ranks may share one GPU, the bytes moved
 by RCCL's own socket transport (transport.rccl_net_env).
@@ -248,6 +248,31 @@ def main():
                     case += 1
                 check("scan", dtype, op, 5000, "host" if (case + rank) % 2 == 0 else "device", tag=name)
                 case += 1
+    elif suite == "sliced":
+        # the slice schedule (mvx_stage.c: blocking calls at p > 1 from
+        # MVX_SLICE_MIN_MIB on, every rank in the same slices whatever its
+        # buffers' kind) at test sizes -- a 1 MiB threshold, 1 MiB slices --
+        # with the kinds mixed between the ranks as in "mixed", and every
+        # rank on host buffers, then every rank on device buffers
+        os.environ["MVX_SLICE_MIN_MIB"] = "1"
+        os.environ["MVX_SLICE_MIB"] = "1"
+        case = 0
+        for op, dtype in [(102, 10), (111, 17), (105, 8), (103, 6), (100, 11)]:
+            E = mvx.dtype_info(dtype)[0]
+            for how in ("mixed", "host", "device"):
+                def where():
+                    return how if how != "mixed" else ("host" if (case + rank) % 2 == 0 else "device")
+                for n in ((1 << 20) // E + 1, (3 << 20) // E + 7):
+                    check("ar", dtype, op, n, where(), tag="sliced")
+                    case += 1
+                check("red", dtype, op, (5 << 20) // (2 * E) + 3, where(), root=world - 1, tag="sliced")
+                case += 1
+                base = (3 << 20) // E // world
+                check("rs", dtype, op, [base + (q % 3) for q in range(world)], where(), tag="sliced")
+                case += 1
+                check("scan", dtype, op, (2 << 20) // E + 5, where(), tag="sliced")
+                case += 1
+        del os.environ["MVX_SLICE_MIN_MIB"], os.environ["MVX_SLICE_MIB"]
     else:
         # the BASELINE multi-GPU shapes at full size: C3, C4 (p = 4 in the
         # config; any p here), C5

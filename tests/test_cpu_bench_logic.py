@@ -93,12 +93,13 @@ def test_mismatched_world_exits_nonzero_before_any_gpu_work():
     assert "WORLD_SIZE=2" in p.stderr and not p.stdout.strip()
 
 
-def test_self_launch_refuses_more_rccl_ranks_than_gpus():
-    """Without a GPU (this container) --gpus 2 over RCCL cannot place its
-    ranks: the launcher says so and exits 2 before starting workers."""
+def test_self_launch_refuses_more_rccl_ranks_than_gpus(tmp_path):
+    """A topology with no GPU node (a CPU-only KFD tree): --gpus 2 over RCCL
+    cannot place its ranks, so the launcher says so and exits 2 before
+    starting workers."""
     import subprocess
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
-    env["HIP_VISIBLE_DEVICES"] = env.get("HIP_VISIBLE_DEVICES", "")
+    env["MVX_KFD_NODES"] = _fake_kfd(tmp_path, [{"simd_count": 0}])
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"], env=env,
                        capture_output=True, text=True, timeout=120)
     assert p.returncode == 2, (p.returncode, p.stderr[-2000:])
@@ -129,3 +130,60 @@ def test_auto_variants_leave_graphs_to_the_flag():
     both = bench.auto_variants(bench.parse(["--graphs"]))
     assert both[:5] == eager and all(n.endswith("+g") for n in both[5:]) and len(both) == 10
     assert bench.parse(["--exchange", "pipe+g"]).exchange == "pipe+g"
+
+
+def _fake_kfd(tmp, props):
+    """a KFD topology tree: one node directory per properties dict"""
+    for i, p in enumerate(props):
+        d = tmp / "nodes" / str(i)
+        d.mkdir(parents=True)
+        (d / "properties").write_text("".join("%s %s\n" % kv for kv in p.items()))
+    return str(tmp / "nodes")
+
+
+def test_visible_gpus_from_kfd_topology(tmp_path):
+    """GPU nodes are the ones with SIMDs; ROCR_VISIBLE_DEVICES, then
+    HIP_VISIBLE_DEVICES (indices or GPU-<unique_id>) narrow them"""
+    cpu = {"cpu_cores_count": 64, "simd_count": 0, "unique_id": 0}
+    gpus = [{"cpu_cores_count": 0, "simd_count": 1024, "unique_id": 0x1000 + i} for i in range(8)]
+    root = _fake_kfd(tmp_path, [cpu, cpu] + gpus)
+    assert bench.visible_gpus({}, root) == 8
+    assert bench.visible_gpus({"HIP_VISIBLE_DEVICES": "0,3"}, root) == 2
+    assert bench.visible_gpus({"ROCR_VISIBLE_DEVICES": "1,2,5", "HIP_VISIBLE_DEVICES": "2"}, root) == 1
+    assert bench.visible_gpus({"ROCR_VISIBLE_DEVICES": "GPU-%016x,GPU-%016x" % (0x1003, 0x1004)}, root) == 2
+    assert bench.visible_gpus({"CUDA_VISIBLE_DEVICES": "0,9"}, root) == 1      # stops at the invalid one
+    assert bench.visible_gpus({}, str(tmp_path / "absent")) is None
+
+
+def test_launcher_counts_gpus_without_torch(tmp_path, monkeypatch):
+    """bench.py --gpus N (no launcher, --transport rccl) decides whether the
+    box has N GPUs and starts its workers without importing torch: with torch
+    poisoned in sys.modules, 2 fake GPUs lead to 2 Popen calls, 1 fake GPU to
+    exit code 2 and none."""
+    import subprocess
+    import types
+    root = _fake_kfd(tmp_path, [{"simd_count": 0}] + [{"simd_count": 1024, "unique_id": i + 1} for i in range(2)])
+    monkeypatch.setitem(sys.modules, "torch", None)      # `import torch` raises ImportError
+    monkeypatch.setenv("MVX_KFD_NODES", root)
+    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(var, raising=False)
+    started = []
+
+    class FakeProc:
+        def __init__(self, cmd, env=None, stdout=None, preexec_fn=None):
+            started.append(env["RANK"])
+            self.returncode = 0
+            self.stdout = types.SimpleNamespace(read=lambda: b"")
+
+        def poll(self):
+            return 0
+
+        def kill(self):
+            pass
+
+    monkeypatch.setattr(subprocess, "Popen", FakeProc)
+    args = types.SimpleNamespace(transport="rccl", launch_grace=1.0)
+    assert bench.launch(args, 2, ["--gpus", "2"]) == 0
+    assert started == ["0", "1"]
+    started.clear()
+    assert bench.launch(args, 3, ["--gpus", "3"]) == 2 and started == []

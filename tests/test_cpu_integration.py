@@ -12,7 +12,13 @@ libmvx_embed.so.  Checks, without a GPU:
     permanent types pass by handle, a node whose bounds disagree is refused;
   * op translation: predefined ops pass by handle, a user op is registered
     once per (handle, function, commute);
-  * host buffers take MVAPICH's own path (the stand-in counts the calls).
+  * host buffers take MVAPICH's own path (the stand-in counts the calls);
+  * the route is agreed across ranks (2-3 processes, the harness's board
+    world): host buffers everywhere run MVAPICH's path on every rank after one
+    route agreement per call (none for an empty call or under
+    MVX_SHIM_ROUTE=local); a rank that wants libmvx takes every rank there,
+    and a twin that cannot be created (no GPU here) fails the call on every
+    rank alike, promptly, and stays failed.
 """
 import ctypes
 import os
@@ -32,8 +38,13 @@ FLOAT_INT, LB, UB = 17, 15, 16
 MPI_SUM, MPI_MAXLOC, MPI_ERR_TYPE = 102, 111, 3
 
 
-def _lib(smp=False):
+def _lib(smp=False, init=True):
     subprocess.check_call(["make", "-s", "-C", CHECK])
+    # the package loads torch (if present) before libmvx*, so one HIP runtime
+    # serves both: loaded first, the check library's libamdhip64.so.7 would
+    # leave torch a second runtime that knows none of our pointers
+    import importlib
+    importlib.import_module("mvapich-cce_amd").coll()
     so = os.path.join(CHECK, "libintra_mvx_check_smp.so" if smp else "libintra_mvx_check.so")
     lib = ctypes.CDLL(so)
     vp, lg, i = ctypes.c_void_p, ctypes.c_long, ctypes.c_int
@@ -54,7 +65,8 @@ def _lib(smp=False):
     lib.h_reduce.argtypes = [vp, vp, i, vp, i, i]
     lib.h_reduce_scatter.argtypes = [vp, vp, vp, vp, i]
     lib.h_scan.argtypes = [vp, vp, i, vp, i]
-    assert lib.h_init() == 0
+    if init:
+        assert lib.h_init() == 0
     return lib
 
 
@@ -261,3 +273,67 @@ def test_check_headers_match_reference_layout():
     assert int(names["comm_t.collops"]) > int(dict(lay["plain"])["comm_t.collops"])
     with open(os.path.join(os.path.dirname(rl.__file__), "ref_layout.h")) as f:
         assert f.read() == rl.header_text(lay)
+
+
+def _world(np_, scenario, envs=None, timeout=120):
+    """np_ shim_worker.py processes sharing one harness board; their reports"""
+    import json
+    import sys
+    import tempfile
+    d = tempfile.mkdtemp(prefix="mvx_shim_")
+    board = os.path.join(d, "board")
+    with open(board, "wb") as f:
+        f.write(b"\0" * 16384)
+    procs = []
+    for r in range(np_):
+        env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+        env.pop("MVX_HOST_BUFFERS", None)
+        env.pop("MVX_SHIM_ROUTE", None)
+        env.update((envs or {}).get(r, {}))
+        procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "shim_worker.py"), str(r),
+                                       str(np_), board, os.path.join(d, "r%d.json" % r), scenario], env=env))
+    try:
+        rcs = [p.wait(timeout=timeout) for p in procs]
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    assert rcs == [0] * np_, rcs
+    reps = []
+    for r in range(np_):
+        with open(os.path.join(d, "r%d.json" % r)) as f:
+            reps.append(json.load(f))
+    return reps
+
+
+@pytest.mark.parametrize("np_", [2, 3])
+def test_route_agreed_host_buffers_everywhere(mvx, np_):
+    """Host buffers on every rank: every call runs MVAPICH's own function on
+    every rank, after exactly one route agreement; an empty call and
+    MVX_SHIM_ROUTE=local agree nothing."""
+    for rep in _world(np_, "route"):
+        calls = {c["name"]: c for c in rep["calls"]}
+        for name in ("allreduce", "reduce", "reduce_scatter", "scan", "allreduce_again"):
+            assert calls[name] == dict(calls[name], rc=0, agree=1, host=1), (rep["rank"], name, calls[name])
+        assert calls["empty"]["agree"] == 0 and calls["empty"]["rc"] == 0
+        assert calls["local"] == dict(calls["local"], rc=0, agree=0, host=1), calls["local"]
+
+
+def test_route_one_rank_wanting_libmvx_takes_every_rank(mvx):
+    """MVX_HOST_BUFFERS=1 on rank 0 only (the rank-local rule would send rank
+    0 to libmvx and rank 1 to MVAPICH's path: a hang).  Agreed, every rank
+    goes to libmvx; with no GPU here the twin cannot be created, so every
+    rank fails the call (MPI_ERR_OTHER) without entering RCCL, within
+    seconds, and every later call fails the same way with no second
+    creation attempt (one route agreement per call, no creation
+    agreements)."""
+    reps = _world(2, "want", {0: {"MVX_HOST_BUFFERS": "1"}})
+    for rep in reps:
+        first, *rest = rep["calls"]
+        assert first["rc"] == 15 and first["host"] == 0, rep
+        # route + the creation agreement (device check / id) that stopped it
+        assert first["agree"] == 2, first
+        assert first["s"] < 30, first
+        for c in rest:
+            assert c["rc"] == 15 and c["host"] == 0 and c["agree"] == 1, c

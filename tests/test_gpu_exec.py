@@ -197,8 +197,9 @@ def test_argument_test_order(mvx):
 @pytest.mark.parametrize("p", [2, 3, 4, 8, 9])
 def test_pipelined_exchange_matches_reference(mvx, oracle, slices, p):
     """MVX_EXCH_PIPE: slice t's exchange while slice t-1 combines on a
-    second stream, then one distribution group (per-slice groups for a
-    non-root Reduce's temporary results); loopback transport here, the RCCL
+    second stream, then one unsliced distribution group on every rank (a
+    non-root Reduce's temporary result included: it is kept whole in one
+    shared temporary); loopback transport here, the RCCL
     executor's phase code -- same bits as the reference schedule for every
     collective, role-sensitive ops included."""
     import torch

@@ -2,15 +2,25 @@
 MVAPICH's dreg, mpid/ch_gen2/dreg.c:774-832).
 
 With the cache on, a pageable range a call uses is page-locked on first use
-and found again on later calls (hits), so those DMA directly.  A registered
-buffer that is unregistered (mvx_host_unregister, the contract), freed and
-reallocated at the same size must still reduce bit-exact.  Without the call
-the next DMA through the stale registration faulted the GPU (measured once
-in round 4; never run again).  Every test leaves its
-registrations dropped before its buffers are freed (the fixture turns the
-cache off, which unregisters everything).  Results are checked against
-numpy (sums of small integers in float32 are exact).
+and found again on later calls (hits), so those DMA directly.
+
+A registration must not outlive its memory: in round 4 a DMA through a
+registration whose buffer had been freed and allocated again at the same
+address faulted the GPU.  libmvx.so now interposes the calls that release
+memory (free, realloc, munmap, mremap, madvise, sbrk) and drops the
+registrations inside a released range first (the reference's mem_hooks.c).
+test_free_and_reallocate_without_unregister runs that case in a C program
+linked with -lmvx (tests/reg_app.c: free and munmap with no unregister call,
+the same addresses handed out again), which checks the entries are gone
+before it makes the second DMA.  This Python process loads libmvx.so with
+ctypes, where the hooks are not the process's (mode 2 of the cache: the test
+unregisters before it frees).  Results are checked against numpy or the CPU
+(sums of small integers in float32 are exact).
 """
+import os
+import subprocess
+import tempfile
+
 import ctypes
 import importlib
 
@@ -72,10 +82,31 @@ def test_repeat_calls_hit_the_cache(mvx, mib):
     assert mvx.host_unregister(a) != 0          # nothing left at that address
 
 
+def test_free_and_reallocate_without_unregister():
+    """A C program linked with -lmvx (cache mode 1, the release hooks in
+    effect): two registered 96 MiB malloc'd buffers freed with no
+    mvx_host_unregister, the same size allocated again, reduced again --
+    bit-exact, and the hooks dropped the stale registrations before the
+    second DMA (the program stops before that DMA otherwise).  The same for
+    mmap'd buffers unmapped and mapped again at the same address."""
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    out = os.path.join(tempfile.mkdtemp(prefix="mvx_reg_"), "reg_app")
+    pkg = os.path.join(root, "mvapich-cce_amd")
+    subprocess.check_call(["gcc", "-O2", "-std=gnu99", "-Wall", "-Werror", "-D__HIP_PLATFORM_AMD__",
+                           "-I/opt/rocm/include", "-I" + os.path.join(root, "include"),
+                           os.path.join(here, "reg_app.c"), "-o", out, "-L" + pkg, "-lmvx",
+                           "-L/opt/rocm/lib", "-lamdhip64", "-Wl,-rpath," + pkg, "-Wl,-rpath,/opt/rocm/lib"])
+    env = {k: v for k, v in os.environ.items() if not k.startswith("MVX_HOST_REGISTER")}
+    p = subprocess.run([out, "gpu"], capture_output=True, text=True, timeout=120, env=env)
+    assert p.returncode == 0 and "reg_app ok" in p.stdout, p.stdout[-2000:] + p.stderr[-2000:]
+    print(p.stdout)
+
+
 def test_free_and_reallocate_same_size(mvx):
-    """A registered buffer is unregistered, freed and the same size
-    allocated again (the same address in practice); the call on the new
-    buffer must see its new contents."""
+    """Mode 2 (this process's contract): a registered buffer is
+    unregistered, freed and the same size allocated again (the same address
+    in practice); the call on the new buffer must see its new contents."""
     n = 96 * MIB // 4
     libc, px = _libc_buffer(n * 4)
     _, py = _libc_buffer(n * 4)

@@ -7,6 +7,12 @@ must be the reference's for one rank (recvbuf = sendbuf's type-map bytes,
 bytes outside the type map untouched), the attribute's delete callback must
 free the twin, and MVX_HOST_BUFFERS=1 must route host buffers to libmvx.
 User functions must see the caller's datatype handle (mvx_type_set_handle).
+
+Across processes (the harness's board world, RCCL over its socket transport
+with the ranks sharing the GPU): rank 0 passes device buffers and the others
+host buffers in the same call -- every rank must go to libmvx (the route is
+agreed) and get the reference's bits; and a rank whose device cannot be used
+(MVX_DEVICE_ID out of range) must make every rank's call fail, not hang.
 """
 import ctypes
 
@@ -14,7 +20,7 @@ import numpy as np
 import pytest
 
 import uops
-from test_cpu_integration import FLOAT, INT, DOUBLE, UB, MPI_SUM, UNSIGNED, Nodes, _lib
+from test_cpu_integration import FLOAT, INT, DOUBLE, UB, MPI_SUM, UNSIGNED, Nodes, _lib, _world
 
 pytestmark = pytest.mark.gpu
 
@@ -128,3 +134,31 @@ def test_user_function_sees_callers_handle(mvx, where):
         comm.free()
         mvx.MPI_Op_free(op)
         mvx.MPI_Type_free(t)
+
+
+@pytest.mark.parametrize("np_", [2, 3])
+def test_mixed_buffer_kinds_through_the_shim(mvx, np_):
+    """Rank 0 device buffers, the other ranks host buffers, one call: the
+    agreed route takes every rank to libmvx (the host ranks through its HBM
+    mirrors), no rank runs MVAPICH's path, and every rank's recvbuf is the
+    oracle's replay of the reference schedule bit for bit -- Allreduce,
+    Reduce (root np-1), Reduce_scatter (ragged counts) and Scan."""
+    for rep in _world(np_, "mixed", timeout=300):
+        assert not rep["fails"], rep
+        assert len(rep["calls"]) == 4
+        for c in rep["calls"]:
+            assert c["rc"] == 0 and c["host"] == 0, c
+        # the first call agreed the route and created the twin (two MIN
+        # agreements); later calls agree the route only
+        assert rep["calls"][0]["agree"] == 3 and all(c["agree"] == 1 for c in rep["calls"][1:]), rep
+
+
+def test_twin_creation_failure_on_one_rank_fails_every_rank(mvx):
+    """Rank 1's device is unusable (MVX_DEVICE_ID=99): the creation agreement
+    stops every rank before RCCL's collective init, so both ranks return
+    MPI_ERR_OTHER within seconds, and keep returning it."""
+    reps = _world(2, "fail", {1: {"MVX_DEVICE_ID": "99"}}, timeout=180)
+    for rep in reps:
+        assert len(rep["calls"]) == 4
+        for c in rep["calls"]:
+            assert c["rc"] == 15 and c["host"] == 0 and c["s"] < 30, (rep["rank"], c)

@@ -137,6 +137,20 @@ def test_mixed_buffer_kinds_across_ranks(world, transport):
         assert not rep["fails"], rep["fails"][:5]
 
 
+@pytest.mark.parametrize("world,transport", [(2, "host"), (3, "host"), (2, "rccl-net"), (4, "rccl-net")])
+def test_slice_schedule_any_kinds(world, transport):
+    """The slice schedule of large blocking calls (a 1 MiB threshold and
+    1 MiB slices here): every rank runs the same slices whatever its
+    buffers' kind -- host ranks overlapping H2D / collective / D2H, device
+    ranks issuing slices back to back -- so mixed kinds pair; all host and
+    all device too; every collective, role-sensitive ops included,
+    bit-exact against the oracle's replay."""
+    for rep in _launch(world, transport, "sliced", 600):
+        assert rep["checked"] >= 5 * 3 * 5
+        assert not rep["fails"], rep["fails"][:5]
+        assert set(rep["ran"]["sliced"]) <= {"0", "-1"}, rep["ran"]     # P2P slices
+
+
 @pytest.mark.parametrize("world", [2, 4])
 def test_graphs_rccl_net(world):
     """HIP graphs of RCCL device calls (mvx_comm_set_graphs) on RCCL
