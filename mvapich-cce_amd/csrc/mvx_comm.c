@@ -145,6 +145,9 @@ static void exchange_from_env(mvx_comm_t *c)
     c->exch_slices = 4;
     c->host_sliced = env_int("MVX_HOST_PIPELINE", &v) && v == 1;
     c->graphs = env_int("MVX_GRAPH", &v) && v == 1;
+    c->graph_cap = GRAPH_CACHE;
+    if (env_int("MVX_GRAPH_CACHE", &v) && v >= 1 && v <= GRAPH_CACHE) c->graph_cap = v;
+    c->graph_evict = env_int("MVX_GRAPH_EVICT", &v) && v == 1;
     if (!e) return;
     if (!strncmp(e, "pipe", 4)) {
         c->exch = MVX_EXCH_PIPE;
@@ -684,7 +687,7 @@ int mvx_comm_reserve(MPI_Comm comm, size_t bytes)
     if (!c) return ERR_COMM_NULL_CODE;
     mvx_comm_reap();
     if ((prev = mvxi_dev_enter(c->device)) == MVXI_DEV_FAILED) return MPI_ERR_OTHER;
-    rc = mvxi_grow(&c->pool, &c->pool_bytes, bytes);
+    rc = mvxi_grow_pool(c, bytes);
     mvxi_dev_leave(c->device, prev);
     return rc;
 }

@@ -249,7 +249,7 @@ int mvxi_job_layout(mvx_comm_t *c, rank_exec_t *X, const job_t *J, const mvx_pla
     size_t off[MVX_MAXP];
     const size_t need = mvxi_region_layout(c, X, J, Q, off);
     int r, rc;
-    if ((rc = mvxi_grow(&c->pool, &c->pool_bytes, need))) return rc;
+    if ((rc = mvxi_grow_pool(c, need))) return rc;
     for (r = 0; r < J->nr; r++) X[r].pool = c->pool + off[r];
     return MPI_SUCCESS;
 }
@@ -371,7 +371,7 @@ static int run_device_pipe_on(mvx_comm_t *c, const job_t *J, hipStream_t st)
         X0[r].recvbuf = J->recv[r];
     }
     region = mvxi_region_layout(c, X0, J, pl[0], off);   /* slice 0 is the largest */
-    if ((rc = mvxi_grow(&c->pool, &c->pool_bytes, (size_t)nsl * region + tmp_bytes))) return rc;
+    if ((rc = mvxi_grow_pool(c, (size_t)nsl * region + tmp_bytes))) return rc;
     if ((rc = mvxi_tev(c, 0, st))) return rc;
     for (t = 0; t < nsl; t++) {
         const int k = (int)(t & 1);
@@ -450,7 +450,7 @@ static int run_device_coll(mvx_comm_t *c, const job_t *J, long b, hipStream_t st
     stage = al256(bb * (size_t)P->p);
     X.wide_n = mvxi_wide_temps(P);
     X.wide_slot = al256(bb + SLOT_STAGGER);
-    if ((rc = mvxi_grow(&c->pool, &c->pool_bytes, stage + X.wide_slot * (size_t)X.wide_n))) return rc;
+    if ((rc = mvxi_grow_pool(c, stage + X.wide_slot * (size_t)X.wide_n))) return rc;
     c->ran_exch = MVX_EXCH_COLL;
     if ((rc = mvxi_tev(c, 0, st))) return rc;
     if ((rc = t->alltoall(t, J->send[0], c->pool, bb, st))) return rc;
@@ -520,7 +520,11 @@ static int graph_match(const graph_ent_t *g, const mvx_comm_t *c, const job_t *J
  * before mvx_comm_free (mvxi_graphs_clear, run before ncclCommDestroy): a
  * graph whose pool was reallocated is retired (state 3, never matched
  * again), seen-once entries are the only ones replaced, and a communicator
- * that has captured GRAPH_CACHE graphs runs its new jobs eagerly. */
+ * that has captured GRAPH_CACHE graphs runs its new jobs eagerly.
+ * MVX_GRAPH_EVICT=1 destroys them mid-life again (graphs on a pool about to
+ * be freed, before the free; the least recently used one when every slot
+ * holds a graph), and MVX_GRAPH_CACHE=n (<= 32) caps the graphs a
+ * communicator holds -- the round-5 reproduction of the crash. */
 
 static void graph_destroy(graph_ent_t *g)
 {
@@ -536,6 +540,31 @@ void mvxi_graphs_clear(mvx_comm_t *c)
     int i;
     if (!c->w) return;
     for (i = 0; i < GRAPH_CACHE; i++) graph_destroy(&c->w->graphs[i]);
+}
+
+/* The pool is about to be freed: every graph captured on it goes first --
+ * destroyed (graph_evict; after the device drained, so no launch of it is
+ * in flight) or retired (kept, never matched again, destroyed with the
+ * communicator). */
+int mvxi_grow_pool(mvx_comm_t *c, size_t need)
+{
+    int i;
+    if (need <= c->pool_bytes) return MPI_SUCCESS;
+    if (c->w && c->pool && !mvxi_capturing) {
+        int live = 0;
+        for (i = 0; i < GRAPH_CACHE; i++) {
+            graph_ent_t *g = &c->w->graphs[i];
+            if (g->pool != c->pool) continue;
+            if (g->state == G_SEEN) memset(g, 0, sizeof *g);
+            else if (g->state == G_LIVE) { g->state = G_RETIRED; live++; }
+        }
+        if (live && c->graph_evict) {
+            hipDeviceSynchronize();
+            for (i = 0; i < GRAPH_CACHE; i++)
+                if (c->w->graphs[i].state == G_RETIRED) graph_destroy(&c->w->graphs[i]);
+        }
+    }
+    return mvxi_grow(&c->pool, &c->pool_bytes, need);
 }
 
 /* MVX_GRAPH_FORK=0: PIPE (whose capture forks to the combine stream and
@@ -569,10 +598,17 @@ static int graph_streams(mvx_comm_t *c)
 
 static int graph_launch(mvx_comm_t *c, hipGraphExec_t x, hipStream_t st)
 {
-    if (st) return hipGraphLaunch(x, st) == hipSuccess ? MPI_SUCCESS : MPI_ERR_OTHER;
-    if (hipEventRecord(c->gev[0], st) != hipSuccess || hipStreamWaitEvent(c->gstream, c->gev[0], 0) != hipSuccess ||
-        hipGraphLaunch(x, c->gstream) != hipSuccess || hipEventRecord(c->gev[1], c->gstream) != hipSuccess ||
-        hipStreamWaitEvent(st, c->gev[1], 0) != hipSuccess)
+    if (st) {
+        gtrace("launch on the caller's stream", 0);
+        return hipGraphLaunch(x, st) == hipSuccess ? MPI_SUCCESS : MPI_ERR_OTHER;
+    }
+    gtrace("launch: fork from the null stream", 0);
+    if (hipEventRecord(c->gev[0], st) != hipSuccess || hipStreamWaitEvent(c->gstream, c->gev[0], 0) != hipSuccess)
+        return MPI_ERR_OTHER;
+    gtrace("launch: hipGraphLaunch on the graph stream", 0);
+    if (hipGraphLaunch(x, c->gstream) != hipSuccess) return MPI_ERR_OTHER;
+    gtrace("launch: join to the null stream", 0);
+    if (hipEventRecord(c->gev[1], c->gstream) != hipSuccess || hipStreamWaitEvent(st, c->gev[1], 0) != hipSuccess)
         return MPI_ERR_OTHER;
     return MPI_SUCCESS;
 }
@@ -629,15 +665,20 @@ static int run_device_graph(mvx_comm_t *c, const job_t *J, hipStream_t st)
     graph_ent_t *g = NULL, *slot = NULL;
     hipGraphExec_t x;
     int i, rc;
+    graph_ent_t *lru = NULL;
     if (!w || (!st && graph_streams(c))) return run_device_eager(c, J, st);
-    for (i = 0; i < GRAPH_CACHE; i++) {
+    for (i = 0; i < c->graph_cap; i++) {
         graph_ent_t *e = &w->graphs[i];
         if (graph_match(e, c, J, st, h)) { g = e; break; }
-        if (e->state == G_LIVE && e->pool != c->pool) e->state = G_RETIRED;   /* made on a freed pool */
-        if (e->state == G_SEEN && e->pool != c->pool) e->state = G_FREE;
         /* a slot for a new job: a free one, else the least recently seen-once */
         if (e->state == G_FREE && (!slot || slot->state != G_FREE)) slot = e;
         else if (e->state == G_SEEN && (!slot || (slot->state == G_SEEN && e->stamp < slot->stamp))) slot = e;
+        if (e->state == G_LIVE && (!lru || e->stamp < lru->stamp)) lru = e;
+    }
+    if (!g && !slot && lru && c->graph_evict) {                /* every slot holds a graph: evict the LRU */
+        hipDeviceSynchronize();
+        graph_destroy(lru);
+        slot = lru;
     }
     if (g && g->state == G_LIVE) {                             /* replay */
         g->stamp = ++w->graph_clock;

@@ -187,6 +187,9 @@ typedef struct {
     int ran_exch;
     unsigned long stamp;
 } graph_ent_t;
+/* the communicator's staging pool grows to `need` bytes; graphs captured on
+ * the old pool are destroyed (or retired) before it is freed (mvx_exec.c) */
+MVXI int mvxi_grow_pool(struct mvx_comm_t *c, size_t need);
 
 /* a capture is open on this thread: staging must not be reallocated */
 extern __thread int mvxi_capturing MVXI;
@@ -243,6 +246,8 @@ struct mvx_comm_t {
     int ran_exch;               /* the variant the last call ran (mvx_comm_last_exchange), -1 none */
     hipStream_t last_st;        /* the stream of the last call (an abort's drain check) */
     int graphs;                 /* mvx_comm_set_graphs: capture / replay device calls */
+    int graph_cap;              /* graphs it may hold (MVX_GRAPH_CACHE, <= GRAPH_CACHE) */
+    int graph_evict;            /* 1: destroy graphs mid-life (LRU, pool change); 0: keep them */
     int graph_error;            /* a capture failed: graphs stay off on this communicator */
     int last_graph;             /* the last call: 0 eager, 1 replayed, 2 captured and launched */
     hipStream_t gstream;        /* graphs of null-stream calls run here (fork / join) */

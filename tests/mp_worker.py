@@ -24,6 +24,9 @@ sys.path[:0] = [ROOT, HERE]
 def main():
     import faulthandler
     faulthandler.enable()           # a crash in native code names the Python line it came from
+    if os.environ.get("MVX_SEGV_BT") == "1":      # ... and the native frames (tools/segv_bt.c)
+        import ctypes
+        ctypes.CDLL(os.path.join(ROOT, "tools", "libsegv_bt.so")).segv_bt_install()
     rank, world, port, out, transport, suite = (int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4],
                                                  sys.argv[5], sys.argv[6])
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=port)

@@ -43,10 +43,11 @@ def _ngpus():
     return torch.cuda.device_count()
 
 
-def _launch(world, transport, suite, timeout):
+def _launch(world, transport, suite, timeout, extra_env=None):
     out = tempfile.mkdtemp(prefix="mvx_mp_")
     port = str(_port())
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    env.update(extra_env or {})
     procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "mp_worker.py"), str(r), str(world), port,
                                os.path.join(out, "r%d.json" % r), transport, suite], env=env)
              for r in range(world)]
@@ -167,6 +168,23 @@ def test_graphs_rccl_net(world):
             # mvx_comm_free, csrc/mvx_exec.c)
             assert all(st in ([0, 2, 1], [0, 0, 0]) for st in runs), (key, runs)
         assert sum(st == [0, 2, 1] for runs in rep["graph_states"].values() for st in runs) >= 16
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_graphs_rccl_net_evicting(world):
+    """The same with graphs destroyed mid-life again (MVX_GRAPH_EVICT=1):
+    at most 4 per communicator (MVX_GRAPH_CACHE=4), so every new job evicts
+    the least recently used graph, and every graph captured on a staging
+    pool about to be freed is destroyed before the free.  Round 4's
+    hipGraphLaunch SIGSEGV came after such destroys; a crash here prints the
+    native stack (MVX_SEGV_BT=1, tools/segv_bt.c)."""
+    env = {"MVX_GRAPH_EVICT": "1", "MVX_GRAPH_CACHE": "4", "MVX_SEGV_BT": "1"}
+    for rep in _launch(world, "rccl-net", "graph", 600, env):
+        assert rep["checked"] > 100
+        assert not rep["fails"], rep["fails"][:5]
+        assert rep["graph_error"] == 0, rep["graph_error"]
+        for key, runs in rep["graph_states"].items():
+            assert all(st == [0, 2, 1] for st in runs), (key, runs)
 
 
 def test_graphs_host_transport_stay_eager():

@@ -30,11 +30,34 @@
  *                           eager RCCL call between the destroy and the
  *                           capture (RCCL reclaims a destroyed graph's plan
  *                           on its next call)
+ *   coll_free_then_destroy  libmvx's round-4 order when its staging pool
+ *                           grew: COLL captured on buffer A, launched; A
+ *                           freed (hipFree) while the exec lives; the exec
+ *                           destroyed; buffer B allocated; COLL eager, then
+ *                           captured on B and launched x3
+ *   coll_destroy_then_free  the same with the exec destroyed before A is
+ *                           freed
+ *   p2p_free_then_destroy   the first order with P2P groups instead of COLL
+ *   null_fork_pipe_cumask   null_fork_pipe with stream 2 made as libmvx
+ *                           makes PIPE's combine stream
+ *                           (hipExtStreamCreateWithCUMask: a blocking
+ *                           stream with a full CU mask) and three forks to
+ *                           it per job, one join (PIPE's shape)
+ *   fork_cumask_stream      the same on a plain capturing stream (no null
+ *                           stream)
+ *   null_fork_{p2p,coll,pipe}  libmvx's blocking (null-stream) path: the
+ *                           job's eager runs on the null stream; its graphs
+ *                           are captured on a second stream (gs) and
+ *                           launched forked from / joined back to the null
+ *                           stream with events; G1 G2 captured and
+ *                           launched, G1's exec destroyed, an eager job on
+ *                           the null stream, then G3 captured and launched
  *
  *   gcc -O2 -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include tools/graph_probe2.c \
  *       -o tools/graph_probe2 -L/opt/rocm/lib -lrccl -lamdhip64
  *   tools/graph_probe2 [scenario ...]      (default: all)
  */
+#include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -56,15 +79,17 @@
 
 static const char *g_names[] = {"coll_after_destroy", "coll_no_destroy", "coll_after_destroy_keep",
                                 "p2p_after_destroy", "coll_then_coll", "fork_after_destroy",
-                                "coll_destroy_sync"};
+                                "coll_destroy_sync", "coll_free_then_destroy", "coll_destroy_then_free",
+                                "p2p_free_then_destroy", "null_fork_p2p", "null_fork_coll", "null_fork_pipe",
+                                "null_fork_pipe_cumask", "fork_cumask_stream"};
 #define NSCEN ((int)(sizeof g_names / sizeof g_names[0]))
 
 typedef struct {
     ncclComm_t comm;
     int rank;
     int *send, *recv, *host;
-    hipStream_t st, s2;
-    hipEvent_t ev[2];
+    hipStream_t st, s2, gs;
+    hipEvent_t ev[2], gev[2];
 } ctx_t;
 
 static void say(int rank, const char *s) { fprintf(stderr, "rank %d: %s\n", rank, s); }
@@ -97,6 +122,21 @@ static int fork_join(ctx_t *c)
     return hipStreamWaitEvent(c->st, c->ev[1], 0) != hipSuccess;
 }
 
+/* PIPE's shape proper: per slice a group on st, a fork to s2 (events
+ * reused by slice parity) and work there; one join at the end */
+static int pipe3(ctx_t *c)
+{
+    int t;
+    for (t = 0; t < 3; t++) {
+        if (p2p(c)) return 1;
+        if (hipEventRecord(c->ev[t & 1], c->st) != hipSuccess || hipStreamWaitEvent(c->s2, c->ev[t & 1], 0) != hipSuccess)
+            return 1;
+        if (hipMemsetAsync(c->send + N / 2 + t, 0, 4, c->s2) != hipSuccess) return 1;
+    }
+    if (hipEventRecord(c->ev[0], c->s2) != hipSuccess || hipStreamWaitEvent(c->st, c->ev[0], 0) != hipSuccess) return 1;
+    return p2p(c);
+}
+
 typedef int (*job_fn)(ctx_t *);
 
 /* capture `job` on st; the graph is destroyed at once unless keep != NULL */
@@ -125,13 +165,49 @@ static int launch(ctx_t *c, hipGraphExec_t x, int times)
     return 0;
 }
 
-static int scenario(ctx_t *c, int s)
+/* the job on a fresh pair of buffers of `bytes` each (c->send / c->recv
+ * pointed at them); the old pair is freed before (free_first) or after the
+ * exec that captured it is destroyed */
+static int realloc_case(ctx_t *c, job_fn job, int free_first)
+{
+    int *a_send, *a_recv, *b_send, *b_recv;
+    hipGraphExec_t g1, g2;
+    int rank = c->rank;
+    CHK(hipMalloc((void **)&a_send, N * sizeof(int)) == hipSuccess && hipMalloc((void **)&a_recv, N * sizeof(int)) == hipSuccess, "malloc a");
+    CHK(hipMemcpy(a_send, c->host, N * sizeof(int), hipMemcpyHostToDevice) == hipSuccess, "h2d a");
+    c->send = a_send; c->recv = a_recv;
+    CHK(job(c) == 0 && hipStreamSynchronize(c->st) == hipSuccess, "eager on a");
+    CHK(capture(c, job, &g1, NULL) == 0, "capture on a");
+    CHK(launch(c, g1, 2) == 0, "launch on a");
+    CHK(hipDeviceSynchronize() == hipSuccess, "sync");
+    if (free_first) {
+        say(rank, "free a, exec alive");
+        hipFree(a_send); hipFree(a_recv);
+        say(rank, "destroy exec of a");
+        hipGraphExecDestroy(g1);
+    } else {
+        say(rank, "destroy exec of a");
+        hipGraphExecDestroy(g1);
+        say(rank, "free a");
+        hipFree(a_send); hipFree(a_recv);
+    }
+    CHK(hipMalloc((void **)&b_send, 2 * N * sizeof(int)) == hipSuccess && hipMalloc((void **)&b_recv, 2 * N * sizeof(int)) == hipSuccess, "malloc b");
+    CHK(hipMemcpy(b_send, c->host, N * sizeof(int), hipMemcpyHostToDevice) == hipSuccess, "h2d b");
+    c->send = b_send; c->recv = b_recv;
+    CHK(job(c) == 0 && hipStreamSynchronize(c->st) == hipSuccess, "eager on b");
+    CHK(capture(c, job, &g2, NULL) == 0, "capture on b");
+    CHK(launch(c, g2, 3) == 0, "launch on b");
+    hipGraphExecDestroy(g2);
+    return 0;
+}
+
+static int scenario_graphs(ctx_t *c, int s)
 {
     hipGraphExec_t g1, g2, g3;
     hipGraph_t k1 = NULL, k2 = NULL, k3 = NULL;
     const int keep = s == 2;
     int rank = c->rank;
-    job_fn last = s == 3 ? p2p : s == 5 ? fork_join : coll;
+    job_fn last = s == 3 ? p2p : s == 5 ? fork_join : s == 15 ? pipe3 : coll;
 
     if (s == 4) {                                   /* coll_then_coll */
         CHK(coll(c) == 0 && hipStreamSynchronize(c->st) == hipSuccess, "eager coll");
@@ -170,6 +246,66 @@ static int scenario(ctx_t *c, int s)
     return 0;
 }
 
+/* a graph launched as libmvx launches one for a null-stream call */
+static int launch_null(ctx_t *c, hipGraphExec_t x, int times)
+{
+    int i, rank = c->rank;
+    for (i = 0; i < times; i++) {
+        say(rank, "launch forked from the null stream");
+        CHK(hipEventRecord(c->gev[0], NULL) == hipSuccess && hipStreamWaitEvent(c->gs, c->gev[0], 0) == hipSuccess,
+            "fork");
+        CHK(hipGraphLaunch(x, c->gs) == hipSuccess, "launch");
+        CHK(hipEventRecord(c->gev[1], c->gs) == hipSuccess && hipStreamWaitEvent(NULL, c->gev[1], 0) == hipSuccess,
+            "join");
+        CHK(hipStreamSynchronize(NULL) == hipSuccess, "null sync");
+    }
+    return 0;
+}
+
+static int null_fork(ctx_t *c, job_fn job)
+{
+    hipGraphExec_t g1, g2, g3;
+    hipStream_t st = c->st;
+    int rank = c->rank;
+    /* eager on the null stream */
+    c->st = NULL;
+    CHK(job(c) == 0 && hipStreamSynchronize(NULL) == hipSuccess, "eager on the null stream");
+    /* captures on gs */
+    c->st = c->gs;
+    CHK(capture(c, job, &g1, NULL) == 0, "capture 1 on gs");
+    CHK(launch_null(c, g1, 2) == 0, "launch 1");
+    CHK(capture(c, job, &g2, NULL) == 0, "capture 2 on gs");
+    CHK(launch_null(c, g2, 2) == 0, "launch 2");
+    say(rank, "destroy exec 1");
+    hipGraphExecDestroy(g1);
+    c->st = NULL;
+    CHK(job(c) == 0 && hipStreamSynchronize(NULL) == hipSuccess, "eager on the null stream after destroy");
+    c->st = c->gs;
+    CHK(capture(c, job, &g3, NULL) == 0, "capture 3 on gs");
+    CHK(launch_null(c, g3, 3) == 0, "launch 3");
+    hipGraphExecDestroy(g3);
+    hipGraphExecDestroy(g2);
+    c->st = st;
+    return 0;
+}
+
+static int scenario(ctx_t *c, int s)
+{
+    if (s == 7 || s == 8) return realloc_case(c, coll, s == 7);
+    if (s == 9) return realloc_case(c, p2p, 1);
+    if (s == 13 || s == 14) {                      /* s2 as PIPE's combine stream */
+        uint32_t mask[16];
+        int rank = c->rank;
+        memset(mask, 0xff, sizeof mask);
+        CHK(hipStreamDestroy(c->s2) == hipSuccess, "destroy s2");
+        CHK(hipExtStreamCreateWithCUMask(&c->s2, 16, mask) == hipSuccess, "cu-mask stream");
+        if (s == 13) return null_fork(c, pipe3);
+        return scenario_graphs(c, 15);
+    }
+    if (s >= 10) return null_fork(c, s == 10 ? p2p : s == 11 ? coll : fork_join);
+    return scenario_graphs(c, s);
+}
+
 static int run(int rank, ncclUniqueId id, int s)
 {
     ctx_t c;
@@ -179,7 +315,9 @@ static int run(int rank, ncclUniqueId id, int s)
     CHK(hipSetDevice(0) == hipSuccess, "hipSetDevice");
     CHK(hipStreamCreateWithFlags(&c.st, hipStreamNonBlocking) == hipSuccess, "stream");
     CHK(hipStreamCreateWithFlags(&c.s2, hipStreamNonBlocking) == hipSuccess, "stream 2");
+    CHK(hipStreamCreateWithFlags(&c.gs, hipStreamNonBlocking) == hipSuccess, "graph stream");
     for (i = 0; i < 2; i++) CHK(hipEventCreateWithFlags(&c.ev[i], hipEventDisableTiming) == hipSuccess, "event");
+    for (i = 0; i < 2; i++) CHK(hipEventCreateWithFlags(&c.gev[i], hipEventDisableTiming) == hipSuccess, "event");
     CHK(hipMalloc((void **)&c.send, N * sizeof(int)) == hipSuccess, "malloc");
     CHK(hipMalloc((void **)&c.recv, N * sizeof(int)) == hipSuccess, "malloc");
     c.host = (int *)malloc(N * sizeof(int));

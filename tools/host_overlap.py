@@ -1,8 +1,9 @@
 """Does a host-buffer rank overlap its PCIe copies with the collective?
 Reads one rank's rocprofv3 output directory (--kernel-trace
 --memory-copy-trace, CSV) and reports the busy time of each stream of work
--- host-to-device copies, device-to-host copies, kernels (RCCL transfers and
-the combines) -- the time covered by any of them, and how much of each ran
+-- host-to-device copies, device-to-host copies (SDMA, or HIP's blit
+kernels, which it used for the slices' D2H), the collective's kernels (RCCL
+transfers and the combines) -- the time covered by any of them, and how much of each ran
 while another kind was running.  overlap_factor = (sum of the three busy
 times) / (time covered by any): 1.0 when they run one after another, up to
 3.0 when all three always run together.  Used by tools/prof_host_multi.sh.
@@ -60,12 +61,19 @@ def main(d, label=""):
             h2d.append(span)
         elif "DEVICE_TO_HOST" in way:
             d2h.append(span)
+    blit = []
     for r in kernels:
-        ker.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
-    H, D, K = union(h2d), union(d2h), union(ker)
+        span = (int(r["Start_Timestamp"]), int(r["End_Timestamp"]))
+        name = r["Kernel_Name"]
+        if "copyBuffer" in name:          # HIP's blit-kernel copies (it ran the slices' D2H this way)
+            blit.append(span)
+        elif "mvx::" in name or "ncclDevKernel" in name or "rccl" in name.lower():
+            ker.append(span)             # the collective: RCCL transfers and the combines
+    H, D, K = union(h2d), union(d2h + blit), union(ker)
     anyb = union(H + D + K)
     tot = length(anyb)
-    res = {"label": label, "h2d_copies": len(h2d), "d2h_copies": len(d2h), "kernels": len(ker),
+    res = {"label": label, "h2d_copies": len(h2d), "d2h_copies": len(d2h), "blit_copies": len(blit),
+           "collective_kernels": len(ker),
            "h2d_ms": round(length(H) / 1e6, 3), "d2h_ms": round(length(D) / 1e6, 3),
            "kernel_ms": round(length(K) / 1e6, 3), "any_ms": round(tot / 1e6, 3),
            "overlap_factor": round((length(H) + length(D) + length(K)) / tot, 3) if tot else None,
