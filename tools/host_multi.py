@@ -82,7 +82,8 @@ def main():
                       "kinds": kinds, "mib": a.mib, "ms": round(ms, 3), "ms_all": [round(t * 1e3, 3) for t in times],
                       "GBs": round(n * 4 / (ms * 1e-3) / 1e9, 2), "parity": ok,
                       "schedule": "sliced" if a.mib >= slice_min else "unsliced",
-                      "slice_mib": int(os.environ.get("MVX_SLICE_MIB", "32")), "transport": a.transport}),
+                      "slice_mib": int(os.environ.get("MVX_SLICE_MIB", "32")), "transport": a.transport,
+                      "exchange_ran": {-1: "none", 0: "p2p", 1: "pipe", 2: "coll"}.get(comm.last_exchange())}),
           flush=True)
     comm.free()
     dist.barrier()
