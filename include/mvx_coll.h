@@ -117,10 +117,19 @@ int mvx_comm_last_exchange(MPI_Comm comm, int *mode);
  * especially).  The first call of a job runs eagerly, the second captures
  * and launches, later ones replay.  Same bits as the eager calls.  A failed
  * capture turns graphs off on the communicator (mvx_comm_last_graph reports
- * the error).  Captured graphs live until mvx_comm_free (at most 32 per
- * communicator; jobs past that run eagerly); mvx_comm_set_graphs(comm, 0)
+ * the error).  A communicator holds at most 32 graphs (MVX_GRAPH_CACHE=n
+ * fewer); when they are all taken the least recently used one is destroyed
+ * for a new job, and graphs captured on a staging pool are destroyed before
+ * the pool is reallocated -- any graph on HIP 7.2 and later, only graphs
+ * without parallel branches on earlier runtimes, where destroying a forked
+ * graph's exec crashes later launches (PIPE's graphs are kept there until
+ * mvx_comm_free, and jobs past the cap run eagerly).  MVX_GRAPH_EVICT=0|1|2
+ * overrides: none / single-branch only / all.  mvx_comm_set_graphs(comm, 0)
  * stops their use without destroying them. */
 int mvx_comm_set_graphs(MPI_Comm comm, int on);
+/* graphs the communicator holds (live: replayable; retired: kept, never
+ * replayed again) and execs destroyed mid-life so far */
+int mvx_comm_graph_stats(MPI_Comm comm, int *live, int *retired, long *destroyed);
 /* The last call: *state 0 eager, 1 replayed, 2 captured and launched;
  * *error the failed capture's code that turned graphs off (0: none). */
 int mvx_comm_last_graph(MPI_Comm comm, int *state, int *error);

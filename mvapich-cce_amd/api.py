@@ -175,6 +175,15 @@ class Comm:
         """Capture device calls into HIP graphs and replay them (mvx_comm_set_graphs)."""
         return coll().mvx_comm_set_graphs(self.handle, 1 if on else 0)
 
+    def graph_stats(self):
+        """{live, retired, destroyed}: graphs held (replayable / kept but never
+        replayed) and execs destroyed mid-life (mvx_comm_graph_stats)."""
+        live, ret, dst = ctypes.c_int(), ctypes.c_int(), ctypes.c_long()
+        rc = coll().mvx_comm_graph_stats(self.handle, ctypes.byref(live), ctypes.byref(ret), ctypes.byref(dst))
+        if rc:
+            raise RuntimeError("mvx_comm_graph_stats rc=%d" % rc)
+        return {"live": live.value, "retired": ret.value, "destroyed": dst.value}
+
     def last_graph(self):
         """(state, error) of the last call (mvx_comm_last_graph): state 0
         eager, 1 replayed, 2 captured and launched; error the failed

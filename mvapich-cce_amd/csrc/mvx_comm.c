@@ -147,7 +147,8 @@ static void exchange_from_env(mvx_comm_t *c)
     c->graphs = env_int("MVX_GRAPH", &v) && v == 1;
     c->graph_cap = GRAPH_CACHE;
     if (env_int("MVX_GRAPH_CACHE", &v) && v >= 1 && v <= GRAPH_CACHE) c->graph_cap = v;
-    c->graph_evict = env_int("MVX_GRAPH_EVICT", &v) && v == 1;
+    c->graph_evict = mvxi_graph_evict_default();
+    if (env_int("MVX_GRAPH_EVICT", &v) && v >= MVX_GRAPH_EVICT_NONE && v <= MVX_GRAPH_EVICT_ALL) c->graph_evict = v;
     if (!e) return;
     if (!strncmp(e, "pipe", 4)) {
         c->exch = MVX_EXCH_PIPE;
@@ -155,6 +156,22 @@ static void exchange_from_env(mvx_comm_t *c)
     } else if (!strcmp(e, "coll")) {
         c->exch = MVX_EXCH_COLL;
     }
+}
+
+/* Which captured graphs may be destroyed mid-life on this HIP runtime.
+ * HIP 7.0 (70051831, the runtime torch 2.10+rocm7.0 bundles) crashes in
+ * hipGraphLaunch once execs of graphs with parallel branches (a fork / join
+ * across streams) have been destroyed -- with no RCCL and no libmvx in the
+ * process, while the same graphs kept alive, and single-branch graphs
+ * destroyed, run clean (tools/graph_probe2.c churn_*);
+ * HIP 7.2 (70226015, the image's /opt/rocm) runs all of it clean.  So from
+ * 7.2 any graph may be destroyed; before it, only single-branch ones.
+ * MVX_GRAPH_EVICT = 0 | 1 | 2 overrides (none / single-branch / all). */
+int mvxi_graph_evict_default(void)
+{
+    int v = 0;
+    if (hipRuntimeGetVersion(&v) != hipSuccess) { (void)hipGetLastError(); return MVX_GRAPH_EVICT_SERIAL; }
+    return v >= 70200000 ? MVX_GRAPH_EVICT_ALL : MVX_GRAPH_EVICT_SERIAL;
 }
 
 /* a new communicator's flavour: MVX_DEVICE names the reference device */

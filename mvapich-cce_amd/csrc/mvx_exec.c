@@ -521,10 +521,17 @@ static int graph_match(const graph_ent_t *g, const mvx_comm_t *c, const job_t *J
  * graph whose pool was reallocated is retired (state 3, never matched
  * again), seen-once entries are the only ones replaced, and a communicator
  * that has captured GRAPH_CACHE graphs runs its new jobs eagerly.
- * MVX_GRAPH_EVICT=1 destroys them mid-life again (graphs on a pool about to
- * be freed, before the free; the least recently used one when every slot
- * holds a graph), and MVX_GRAPH_CACHE=n (<= 32) caps the graphs a
- * communicator holds -- the round-5 reproduction of the crash. */
+ *
+ * Round 5 found the cause: HIP 7.0's hipGraphLaunch crashes after execs of
+ * graphs with parallel branches were destroyed (tools/graph_probe2.c: a
+ * fork / join graph of two memsets, captured, launched and destroyed in a
+ * loop, dies within 30 rounds on HIP 7.0 and never on 7.2; kept alive, or
+ * without the fork, it never dies; no RCCL needed).  So graphs are destroyed
+ * mid-life again -- before the pool they were captured on is freed, and the
+ * least recently used one when every slot holds a graph -- where the runtime
+ * allows (mvxi_graph_evict_default): any graph from HIP 7.2 on, only
+ * single-branch ones before it (PIPE's forked captures are retired there).
+ * MVX_GRAPH_CACHE=n (<= 32) caps the graphs a communicator holds. */
 
 static void graph_destroy(graph_ent_t *g)
 {
@@ -535,6 +542,28 @@ static void graph_destroy(graph_ent_t *g)
     memset(g, 0, sizeof *g);
 }
 
+/* a graph destroyed mid-life (counted for mvx_comm_graph_stats) */
+static void graph_evict(mvx_comm_t *c, graph_ent_t *g)
+{
+    graph_destroy(g);
+    c->w->graphs_destroyed++;
+}
+
+int mvx_comm_graph_stats(MPI_Comm comm, int *live, int *retired, long *destroyed)
+{
+    mvx_comm_t *c = mvxi_get_comm(comm);
+    int i, l = 0, r = 0;
+    if (!c) return ERR_COMM_NULL_CODE;
+    for (i = 0; c->w && i < GRAPH_CACHE; i++) {
+        l += c->w->graphs[i].state == G_LIVE;
+        r += c->w->graphs[i].state == G_RETIRED;
+    }
+    if (live) *live = l;
+    if (retired) *retired = r;
+    if (destroyed) *destroyed = c->w ? c->w->graphs_destroyed : 0;
+    return MPI_SUCCESS;
+}
+
 void mvxi_graphs_clear(mvx_comm_t *c)
 {
     int i;
@@ -542,26 +571,62 @@ void mvxi_graphs_clear(mvx_comm_t *c)
     for (i = 0; i < GRAPH_CACHE; i++) graph_destroy(&c->w->graphs[i]);
 }
 
+/* may this graph's exec be destroyed now (mvxi_graph_evict_default)? */
+static int graph_evictable(const mvx_comm_t *c, const graph_ent_t *g)
+{
+    if (c->graph_evict == MVX_GRAPH_EVICT_ALL) return 1;
+    return c->graph_evict == MVX_GRAPH_EVICT_SERIAL && !g->forked;
+}
+
+/* 1 if the graph has parallel branches: a node with two or more successors,
+ * or two or more roots (what HIP runs on parallel streams) */
+static int graph_forked(hipGraph_t g)
+{
+    size_t ne = 0, nr = 0, i, j;
+    hipGraphNode_t *from, *to;
+    int forked = 0;
+    if (hipGraphGetRootNodes(g, NULL, &nr) != hipSuccess || hipGraphGetEdges(g, NULL, NULL, &ne) != hipSuccess) {
+        (void)hipGetLastError();
+        return 1;                                   /* unknown: treat as forked */
+    }
+    if (nr > 1) return 1;
+    if (!ne) return 0;
+    from = (hipGraphNode_t *)malloc(ne * sizeof *from);
+    to = (hipGraphNode_t *)malloc(ne * sizeof *to);
+    if (!from || !to || hipGraphGetEdges(g, from, to, &ne) != hipSuccess) {
+        (void)hipGetLastError();
+        free(from);
+        free(to);
+        return 1;
+    }
+    for (i = 0; i < ne && !forked; i++)             /* out-degree >= 2 */
+        for (j = i + 1; j < ne && !forked; j++) forked = from[i] == from[j];
+    free(from);
+    free(to);
+    return forked;
+}
+
 /* The pool is about to be freed: every graph captured on it goes first --
- * destroyed (graph_evict; after the device drained, so no launch of it is
- * in flight) or retired (kept, never matched again, destroyed with the
- * communicator). */
+ * destroyed where the runtime allows it (after the device drained, so no
+ * launch of it is in flight), else retired (kept, never matched again,
+ * destroyed with the communicator). */
 int mvxi_grow_pool(mvx_comm_t *c, size_t need)
 {
     int i;
     if (need <= c->pool_bytes) return MPI_SUCCESS;
     if (c->w && c->pool && !mvxi_capturing) {
-        int live = 0;
+        int gone = 0;
         for (i = 0; i < GRAPH_CACHE; i++) {
             graph_ent_t *g = &c->w->graphs[i];
             if (g->pool != c->pool) continue;
             if (g->state == G_SEEN) memset(g, 0, sizeof *g);
-            else if (g->state == G_LIVE) { g->state = G_RETIRED; live++; }
+            else if (g->state == G_LIVE) { g->state = G_RETIRED; gone += graph_evictable(c, g); }
         }
-        if (live && c->graph_evict) {
+        if (gone) {
             hipDeviceSynchronize();
             for (i = 0; i < GRAPH_CACHE; i++)
-                if (c->w->graphs[i].state == G_RETIRED) graph_destroy(&c->w->graphs[i]);
+                if (c->w->graphs[i].state == G_RETIRED && graph_evictable(c, &c->w->graphs[i]))
+                    graph_evict(c, &c->w->graphs[i]);
         }
     }
     return mvxi_grow(&c->pool, &c->pool_bytes, need);
@@ -625,7 +690,7 @@ static void gtrace(const char *what, int v)
 }
 
 /* capture the job on `cs` into an executable graph (nothing runs) */
-static int graph_capture(mvx_comm_t *c, const job_t *J, hipStream_t cs, hipGraphExec_t *out)
+static int graph_capture(mvx_comm_t *c, const job_t *J, hipStream_t cs, hipGraphExec_t *out, int *forked)
 {
     hipGraph_t g = NULL;
     hipError_t e;
@@ -647,8 +712,10 @@ static int graph_capture(mvx_comm_t *c, const job_t *J, hipStream_t cs, hipGraph
         (void)hipGetLastError();
         return rc ? rc : MPI_ERR_OTHER;
     }
+    *forked = graph_forked(g);
     e = hipGraphInstantiate(out, g, NULL, NULL, 0);
     gtrace("instantiate, hip error", (int)e);
+    gtrace("instantiated graph has parallel branches", *forked);
     hipGraphDestroy(g);
     if (e != hipSuccess) {
         (void)hipGetLastError();
@@ -664,7 +731,7 @@ static int run_device_graph(mvx_comm_t *c, const job_t *J, hipStream_t st)
     const unsigned long long h = graph_hash(c, J, st);
     graph_ent_t *g = NULL, *slot = NULL;
     hipGraphExec_t x;
-    int i, rc;
+    int i, rc, forked = 1;
     graph_ent_t *lru = NULL;
     if (!w || (!st && graph_streams(c))) return run_device_eager(c, J, st);
     for (i = 0; i < c->graph_cap; i++) {
@@ -673,11 +740,11 @@ static int run_device_graph(mvx_comm_t *c, const job_t *J, hipStream_t st)
         /* a slot for a new job: a free one, else the least recently seen-once */
         if (e->state == G_FREE && (!slot || slot->state != G_FREE)) slot = e;
         else if (e->state == G_SEEN && (!slot || (slot->state == G_SEEN && e->stamp < slot->stamp))) slot = e;
-        if (e->state == G_LIVE && (!lru || e->stamp < lru->stamp)) lru = e;
+        if (e->state == G_LIVE && graph_evictable(c, e) && (!lru || e->stamp < lru->stamp)) lru = e;
     }
-    if (!g && !slot && lru && c->graph_evict) {                /* every slot holds a graph: evict the LRU */
+    if (!g && !slot && lru) {                                  /* every slot holds a graph: evict the LRU */
         hipDeviceSynchronize();
-        graph_destroy(lru);
+        graph_evict(c, lru);
         slot = lru;
     }
     if (g && g->state == G_LIVE) {                             /* replay */
@@ -699,7 +766,7 @@ static int run_device_graph(mvx_comm_t *c, const job_t *J, hipStream_t st)
         slot->stamp = ++w->graph_clock;
         return MPI_SUCCESS;
     }
-    rc = graph_capture(c, J, st ? st : c->gstream, &x);       /* second sighting: capture */
+    rc = graph_capture(c, J, st ? st : c->gstream, &x, &forked);   /* second sighting: capture */
     if (rc) {
         c->graph_error = rc;
         memset(g, 0, sizeof *g);
@@ -707,6 +774,7 @@ static int run_device_graph(mvx_comm_t *c, const job_t *J, hipStream_t st)
         return run_device_eager(c, J, st);
     }
     g->exec = x;
+    g->forked = forked;
     g->state = G_LIVE;
     g->ran_exch = c->ran_exch;
     g->stamp = ++w->graph_clock;

@@ -185,11 +185,17 @@ typedef struct {
     int exch, slices, keep;
     hipGraphExec_t exec;
     int ran_exch;
+    int forked;                 /* the graph has parallel branches (graph_forked) */
     unsigned long stamp;
 } graph_ent_t;
 /* the communicator's staging pool grows to `need` bytes; graphs captured on
  * the old pool are destroyed (or retired) before it is freed (mvx_exec.c) */
 MVXI int mvxi_grow_pool(struct mvx_comm_t *c, size_t need);
+/* which graph execs may be destroyed mid-life on this HIP runtime (mvx_comm.c) */
+#define MVX_GRAPH_EVICT_NONE 0       /* none: retired, destroyed with the communicator */
+#define MVX_GRAPH_EVICT_SERIAL 1     /* those without parallel branches (HIP < 7.2) */
+#define MVX_GRAPH_EVICT_ALL 2        /* any (HIP >= 7.2) */
+MVXI int mvxi_graph_evict_default(void);
 
 /* a capture is open on this thread: staging must not be reallocated */
 extern __thread int mvxi_capturing MVXI;
@@ -200,6 +206,7 @@ extern __thread int mvxi_capturing MVXI;
 typedef struct mvx_work {
     graph_ent_t graphs[GRAPH_CACHE];           /* captured device calls */
     unsigned long graph_clock;
+    long graphs_destroyed;                     /* execs destroyed mid-life so far */
     mvx_plan call_plan;                        /* mvx_api.c run(): this rank's plan */
     mvx_plan pipe[2][MVX_MAXP];                /* PIPE: slice plans, by slice parity */
     rank_exec_t px0[MVX_MAXP], px[2][MVX_MAXP];
@@ -247,7 +254,7 @@ struct mvx_comm_t {
     hipStream_t last_st;        /* the stream of the last call (an abort's drain check) */
     int graphs;                 /* mvx_comm_set_graphs: capture / replay device calls */
     int graph_cap;              /* graphs it may hold (MVX_GRAPH_CACHE, <= GRAPH_CACHE) */
-    int graph_evict;            /* 1: destroy graphs mid-life (LRU, pool change); 0: keep them */
+    int graph_evict;            /* graphs destroyed mid-life (LRU, pool change): MVX_GRAPH_EVICT_* */
     int graph_error;            /* a capture failed: graphs stay off on this communicator */
     int last_graph;             /* the last call: 0 eager, 1 replayed, 2 captured and launched */
     hipStream_t gstream;        /* graphs of null-stream calls run here (fork / join) */

@@ -228,6 +228,7 @@ def main():
                         key = "%s %s" % (name, via)
                         report["graph_states"].setdefault(key, []).append(states)
             report["graph_error"] = comm.last_graph()[1]
+        report["graph_stats"] = comm.graph_stats()
         comm.set_graphs(False)
     elif suite == "mixed":
         # buffer kinds differing between the ranks of one call (MPI allows

@@ -172,19 +172,28 @@ def test_graphs_rccl_net(world):
 
 @pytest.mark.parametrize("world", [2, 4])
 def test_graphs_rccl_net_evicting(world):
-    """The same with graphs destroyed mid-life again (MVX_GRAPH_EVICT=1):
-    at most 4 per communicator (MVX_GRAPH_CACHE=4), so every new job evicts
-    the least recently used graph, and every graph captured on a staging
-    pool about to be freed is destroyed before the free.  Round 4's
-    hipGraphLaunch SIGSEGV came after such destroys; a crash here prints the
-    native stack (MVX_SEGV_BT=1, tools/segv_bt.c)."""
-    env = {"MVX_GRAPH_EVICT": "1", "MVX_GRAPH_CACHE": "4", "MVX_SEGV_BT": "1"}
+    """The same with at most 4 graphs per communicator (MVX_GRAPH_CACHE=4),
+    so graphs are destroyed mid-life: the least recently used one for each
+    new job, and every one captured on a staging pool before the pool is
+    reallocated -- on this process's HIP runtime (torch's 7.0) only graphs
+    without parallel branches, the forked ones being kept (csrc/mvx_exec.c,
+    DESIGN.md section 6: HIP 7.0 crashes in hipGraphLaunch once forked
+    graphs were destroyed).  Every result bit-exact, the cap held; a crash
+    would print the native stack (MVX_SEGV_BT)."""
+    env = {"MVX_GRAPH_CACHE": "4", "MVX_SEGV_BT": "1"}
     for rep in _launch(world, "rccl-net", "graph", 600, env):
         assert rep["checked"] > 100
         assert not rep["fails"], rep["fails"][:5]
         assert rep["graph_error"] == 0, rep["graph_error"]
         for key, runs in rep["graph_states"].items():
-            assert all(st == [0, 2, 1] for st in runs), (key, runs)
+            assert all(st in ([0, 2, 1], [0, 0, 0]) for st in runs), (key, runs)
+        gs = rep["graph_stats"]
+        assert gs["live"] + gs["retired"] <= 4, gs
+        if rep["hip_runtime"] >= 70200000:
+            assert gs["destroyed"] >= 10, gs
+        # on HIP 7.0 the graphs RCCL's socket transport captures have
+        # parallel branches (its proxy's host stream), so all are kept:
+        # the cap holds and nothing crashes
 
 
 def test_graphs_host_transport_stay_eager():

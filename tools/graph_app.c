@@ -22,13 +22,17 @@
 
 #include "mvx_coll.h"
 
-#define N 70001
+#define N 300000           /* the largest job */
+/* job sizes: the first only by default; MVX_APP_SIZES=k runs k of them
+ * (more distinct jobs: with MVX_GRAPH_CACHE small, more evictions) */
+static const int g_sizes[] = {70001, 32768, 300000, 4096 * 8, 140001, 1000};
 
 static int run(int rank, const char *id)
 {
     MPI_Comm c;
     hipStream_t st;
-    int *ds, *dr, *h, i, v, rep, via, st_g, err;
+    int *ds, *dr, *h, i, v, rep, via, st_g, err, z, nz = 1, n;
+    const char *e = getenv("MVX_APP_SIZES");
     static const int modes[3][2] = {{MVX_EXCH_P2P, 0}, {MVX_EXCH_PIPE, 3}, {MVX_EXCH_COLL, 0}};
     if (hipSetDevice(0) != hipSuccess || hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return 1;
     if (mvx_comm_init(&c, rank, 2, 0, id)) { fprintf(stderr, "rank %d: init\n", rank); return 1; }
@@ -37,22 +41,25 @@ static int run(int rank, const char *id)
     hipMalloc((void **)&dr, N * sizeof(int));
     for (i = 0; i < N; i++) h[i] = rank * 1000 + i % 977;
     hipMemcpy(ds, h, N * sizeof(int), hipMemcpyHostToDevice);
+    if (e && atoi(e) > 1) nz = atoi(e) < 6 ? atoi(e) : 6;
     mvx_comm_set_graphs(c, 1);
+    for (z = 0; z < nz; z++)
     for (v = 0; v < 3; v++) {
+        n = g_sizes[z];
         mvx_comm_set_exchange(c, modes[v][0], modes[v][1]);
         for (via = 0; via < 2; via++)
             for (rep = 0; rep < 3; rep++) {
                 hipMemset(dr, 0, N * sizeof(int));
-                fprintf(stderr, "rank %d: variant %d %s rep %d\n", rank, v, via ? "stream" : "blocking", rep);
+                fprintf(stderr, "rank %d: n %d variant %d %s rep %d\n", rank, n, v, via ? "stream" : "blocking", rep);
                 if (via == 0) {
-                    if (MPI_Allreduce(ds, dr, N, MPI_INT, MPI_SUM, c)) return 1;
+                    if (MPI_Allreduce(ds, dr, n, MPI_INT, MPI_SUM, c)) return 1;
                 } else {
-                    if (mvx_allreduce_async(ds, dr, N, MPI_INT, MPI_SUM, c, st) || hipStreamSynchronize(st))
+                    if (mvx_allreduce_async(ds, dr, n, MPI_INT, MPI_SUM, c, st) || hipStreamSynchronize(st))
                         return 1;
                 }
                 mvx_comm_last_graph(c, &st_g, &err);
                 hipMemcpy(h, dr, N * sizeof(int), hipMemcpyDeviceToHost);
-                for (i = 0; i < N; i++)
+                for (i = 0; i < n; i++)
                     if (h[i] != 1000 + 2 * (i % 977)) {
                         fprintf(stderr, "rank %d: wrong result at %d: %d\n", rank, i, h[i]);
                         return 1;

@@ -45,6 +45,20 @@
  *                           it per job, one join (PIPE's shape)
  *   fork_cumask_stream      the same on a plain capturing stream (no null
  *                           stream)
+ *   copy_then_pipe          G1, G2 = a group plus a device-to-device
+ *                           hipMemcpyAsync (libmvx's one-leaf combines and
+ *                           own-block copies), G1 destroyed, then PIPE's
+ *                           shape captured and launched
+ *   null_copy_then_pipe     the same on the null-stream path
+ *   churn_pipe              200 rounds of: capture PIPE's shape, instantiate,
+ *                           launch, destroy the exec (libmvx with eviction
+ *                           crashed after 40-70 graphs per process)
+ *   churn_fork_norccl       the same with no RCCL call in the graph (a
+ *                           memset on each branch)
+ *   churn_p2p               the same with one group per graph
+ *   churn_fork_keep         churn_fork_norccl without destroying: every
+ *                           exec kept until the end
+ *   churn_single            churn_fork_norccl with no fork (one stream)
  *   null_fork_{p2p,coll,pipe}  libmvx's blocking (null-stream) path: the
  *                           job's eager runs on the null stream; its graphs
  *                           are captured on a second stream (gs) and
@@ -81,7 +95,9 @@ static const char *g_names[] = {"coll_after_destroy", "coll_no_destroy", "coll_a
                                 "p2p_after_destroy", "coll_then_coll", "fork_after_destroy",
                                 "coll_destroy_sync", "coll_free_then_destroy", "coll_destroy_then_free",
                                 "p2p_free_then_destroy", "null_fork_p2p", "null_fork_coll", "null_fork_pipe",
-                                "null_fork_pipe_cumask", "fork_cumask_stream"};
+                                "null_fork_pipe_cumask", "fork_cumask_stream", "copy_then_pipe",
+                                "null_copy_then_pipe", "churn_pipe", "churn_fork_norccl", "churn_p2p",
+                                "churn_fork_keep", "churn_single"};
 #define NSCEN ((int)(sizeof g_names / sizeof g_names[0]))
 
 typedef struct {
@@ -135,6 +151,13 @@ static int pipe3(ctx_t *c)
     }
     if (hipEventRecord(c->ev[0], c->s2) != hipSuccess || hipStreamWaitEvent(c->st, c->ev[0], 0) != hipSuccess) return 1;
     return p2p(c);
+}
+
+/* a group, then a device-to-device copy on the same stream */
+static int p2p_copy(ctx_t *c)
+{
+    if (p2p(c)) return 1;
+    return hipMemcpyAsync(c->send + N / 2, c->recv, 4096, hipMemcpyDeviceToDevice, c->st) != hipSuccess;
 }
 
 typedef int (*job_fn)(ctx_t *);
@@ -207,7 +230,8 @@ static int scenario_graphs(ctx_t *c, int s)
     hipGraph_t k1 = NULL, k2 = NULL, k3 = NULL;
     const int keep = s == 2;
     int rank = c->rank;
-    job_fn last = s == 3 ? p2p : s == 5 ? fork_join : s == 15 ? pipe3 : coll;
+    job_fn last = s == 3 ? p2p : s == 5 ? fork_join : (s == 16 || s == 17) ? pipe3 : coll;
+    job_fn first = s == 16 ? p2p_copy : p2p;
 
     if (s == 4) {                                   /* coll_then_coll */
         CHK(coll(c) == 0 && hipStreamSynchronize(c->st) == hipSuccess, "eager coll");
@@ -220,10 +244,10 @@ static int scenario_graphs(ctx_t *c, int s)
         hipGraphExecDestroy(g2);
         return 0;
     }
-    CHK(p2p(c) == 0 && hipStreamSynchronize(c->st) == hipSuccess, "eager p2p");
-    CHK(capture(c, p2p, &g1, keep ? &k1 : NULL) == 0, "capture p2p 1");
+    CHK(first(c) == 0 && hipStreamSynchronize(c->st) == hipSuccess, "eager p2p");
+    CHK(capture(c, first, &g1, keep ? &k1 : NULL) == 0, "capture p2p 1");
     CHK(launch(c, g1, 2) == 0, "launch p2p 1");
-    CHK(capture(c, p2p, &g2, keep ? &k2 : NULL) == 0, "capture p2p 2");
+    CHK(capture(c, first, &g2, keep ? &k2 : NULL) == 0, "capture p2p 2");
     CHK(launch(c, g2, 2) == 0, "launch p2p 2");
     if (s != 1) {
         say(rank, "destroy exec 1");
@@ -262,7 +286,11 @@ static int launch_null(ctx_t *c, hipGraphExec_t x, int times)
     return 0;
 }
 
-static int null_fork(ctx_t *c, job_fn job)
+static int null_fork2(ctx_t *c, job_fn job, job_fn last);
+
+static int null_fork(ctx_t *c, job_fn job) { return null_fork2(c, job, job); }
+
+static int null_fork2(ctx_t *c, job_fn job, job_fn last)
 {
     hipGraphExec_t g1, g2, g3;
     hipStream_t st = c->st;
@@ -279,9 +307,9 @@ static int null_fork(ctx_t *c, job_fn job)
     say(rank, "destroy exec 1");
     hipGraphExecDestroy(g1);
     c->st = NULL;
-    CHK(job(c) == 0 && hipStreamSynchronize(NULL) == hipSuccess, "eager on the null stream after destroy");
+    CHK(last(c) == 0 && hipStreamSynchronize(NULL) == hipSuccess, "eager on the null stream after destroy");
     c->st = c->gs;
-    CHK(capture(c, job, &g3, NULL) == 0, "capture 3 on gs");
+    CHK(capture(c, last, &g3, NULL) == 0, "capture 3 on gs");
     CHK(launch_null(c, g3, 3) == 0, "launch 3");
     hipGraphExecDestroy(g3);
     hipGraphExecDestroy(g2);
@@ -289,10 +317,61 @@ static int null_fork(ctx_t *c, job_fn job)
     return 0;
 }
 
+/* fork / join with memsets only: no RCCL in the graph */
+static int fork_norccl(ctx_t *c)
+{
+    int t;
+    for (t = 0; t < 3; t++) {
+        if (hipMemsetAsync(c->recv + t, 0, 4, c->st) != hipSuccess) return 1;
+        if (hipEventRecord(c->ev[t & 1], c->st) != hipSuccess || hipStreamWaitEvent(c->s2, c->ev[t & 1], 0) != hipSuccess)
+            return 1;
+        if (hipMemsetAsync(c->send + N / 2 + t, 0, 4, c->s2) != hipSuccess) return 1;
+    }
+    if (hipEventRecord(c->ev[0], c->s2) != hipSuccess || hipStreamWaitEvent(c->st, c->ev[0], 0) != hipSuccess) return 1;
+    return hipMemsetAsync(c->recv + 8, 0, 4, c->st) != hipSuccess;
+}
+
+/* memsets on one stream: a graph with a single branch */
+static int single_norccl(ctx_t *c)
+{
+    int t;
+    for (t = 0; t < 4; t++)
+        if (hipMemsetAsync(c->recv + t, 0, 4, c->st) != hipSuccess) return 1;
+    return 0;
+}
+
+static int churn(ctx_t *c, job_fn job, int rounds, int keep)
+{
+    static hipGraphExec_t kept[256];
+    hipGraphExec_t x;
+    int i, rank = c->rank;
+    char msg[64];
+    CHK(job(c) == 0 && hipStreamSynchronize(c->st) == hipSuccess, "eager");
+    for (i = 0; i < rounds; i++) {
+        if (i % 10 == 0) {
+            snprintf(msg, sizeof msg, "churn round %d", i);
+            say(rank, msg);
+        }
+        CHK(capture(c, job, &x, NULL) == 0, "capture");
+        CHK(hipGraphLaunch(x, c->st) == hipSuccess && hipStreamSynchronize(c->st) == hipSuccess, "launch");
+        if (keep && i < 256) kept[i] = x;
+        else CHK(hipGraphExecDestroy(x) == hipSuccess, "destroy");
+    }
+    for (i = 0; keep && i < rounds && i < 256; i++) hipGraphExecDestroy(kept[i]);
+    return 0;
+}
+
 static int scenario(ctx_t *c, int s)
 {
+    if (s == 17) return churn(c, pipe3, 200, 0);
+    if (s == 18) return churn(c, fork_norccl, 200, 0);
+    if (s == 19) return churn(c, p2p, 200, 0);
+    if (s == 20) return churn(c, fork_norccl, 200, 1);
+    if (s == 21) return churn(c, single_norccl, 200, 0);
     if (s == 7 || s == 8) return realloc_case(c, coll, s == 7);
     if (s == 9) return realloc_case(c, p2p, 1);
+    if (s == 15) return scenario_graphs(c, 16);
+    if (s == 16) return null_fork2(c, p2p_copy, pipe3);
     if (s == 13 || s == 14) {                      /* s2 as PIPE's combine stream */
         uint32_t mask[16];
         int rank = c->rank;
@@ -300,7 +379,7 @@ static int scenario(ctx_t *c, int s)
         CHK(hipStreamDestroy(c->s2) == hipSuccess, "destroy s2");
         CHK(hipExtStreamCreateWithCUMask(&c->s2, 16, mask) == hipSuccess, "cu-mask stream");
         if (s == 13) return null_fork(c, pipe3);
-        return scenario_graphs(c, 15);
+        return scenario_graphs(c, 17);
     }
     if (s >= 10) return null_fork(c, s == 10 ? p2p : s == 11 ? coll : fork_join);
     return scenario_graphs(c, s);
