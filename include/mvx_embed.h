@@ -100,6 +100,20 @@ int mvx_host_register_stats(long *entries, size_t *bytes, long *hits, long *miss
 /* registrations dropped by releases (hooks and mvx_host_invalidate) so far */
 long mvx_host_register_invalidations(void);
 
+/* The buffer kinds of every rank in the next blocking collective call on
+ * `comm`, when the caller has agreed them across ranks (the MVAPICH shim
+ * does, integration/intra_mvx.c): MVX_KINDS_DEVICE -- every rank passes
+ * device memory: large calls keep the unsliced schedule and the exchange
+ * variants; MVX_KINDS_HOST -- every rank passes host memory: host calls of
+ * any size overlap their copies in slices; MVX_KINDS_UNKNOWN (the default,
+ * also "mixed") -- the schedule that pairs with any kind.
+ * Every rank must pass the same value; the next call consumes it.  A call
+ * whose own buffers contradict the hint returns MPI_ERR_BUFFER (1). */
+#define MVX_KINDS_UNKNOWN 0
+#define MVX_KINDS_DEVICE 1
+#define MVX_KINDS_HOST 2
+int mvx_comm_set_call_kinds(int comm, int kinds);
+
 /* device flavour and collective knobs (the reference's _SMP_ collops) */
 typedef struct mvx_tuning {
     int smp;                        /* 1: _SMP_ collops, 0: ch_shmem collops  */

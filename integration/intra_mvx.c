@@ -45,6 +45,9 @@
  *                 buffers agree in kind in every call (the route is this
  *                 rank's own buffer test).
  *   MVX_SHIM_ROUTE must be the same on every rank, like any MVAPICH knob.
+ *   The agreement also tells libmvx when every rank passes device memory
+ *   (mvx_comm_set_call_kinds): large calls then keep the unsliced device
+ *   schedule instead of the slices that pair with host-buffer ranks.
  *
  * Translation, per call, cached:
  *   communicator  the first call routed to libmvx creates the twin, on every
@@ -416,18 +419,29 @@ static int route_local(void)
 
 /* The route of one call, the same on every rank: 1 libmvx, 0 MVAPICH's own
  * function; `empty` (no element on any rank) needs no agreement.  A failed
- * agreement returns -1 with *rc set. */
+ * agreement returns -1 with *rc set.  *kinds: what the agreement learnt of
+ * every rank's buffers (MVX_KINDS_*), for libmvx's choice of schedule. */
 static int route(const void *sendbuf, const void *recvbuf, int empty, struct MPIR_COMMUNICATOR *comm,
-                 int *rc)
+                 int *rc, int *kinds)
 {
     int v[2], all[2];
+    const int dev = mvx_buffer_is_device(sendbuf) || mvx_buffer_is_device(recvbuf);
     const int mine = wants_mvx(sendbuf, recvbuf);
+    *kinds = MVX_KINDS_UNKNOWN;
     if (empty || comm->np == 1 || route_local()) return mine && !empty;
     v[0] = mine;
-    v[1] = !mine;
+    v[1] = !dev;
     *rc = MPIR_intra_collops->Allreduce(v, all, 2, MPIR_GET_DTYPE_PTR(MPI_INT), MPI_MAX, comm);
     if (*rc != MPI_SUCCESS) return -1;
+    /* all[1]: some rank's buffers are host memory */
+    *kinds = !all[1] ? MVX_KINDS_DEVICE : MVX_KINDS_UNKNOWN;
     return all[0] != 0;
+}
+
+/* hand the agreed kinds to libmvx for the call about to be made on h */
+static void pass_kinds(int h, int kinds)
+{
+    if (kinds != MVX_KINDS_UNKNOWN) mvx_comm_set_call_kinds(h, kinds);
 }
 
 /* communicator, datatype and op in libmvx's handles */
@@ -444,45 +458,49 @@ static int translate(struct MPIR_COMMUNICATOR *comm, struct MPIR_DATATYPE *dt, M
 static int mvx_Reduce(void *sendbuf, void *recvbuf, int count, struct MPIR_DATATYPE *dt, MPI_Op op,
                       int root, struct MPIR_COMMUNICATOR *comm)
 {
-    int h, t, o, rc = MPI_SUCCESS;
-    const int r = route(sendbuf, recvbuf, count == 0, comm, &rc);
+    int h, t, o, rc = MPI_SUCCESS, kinds;
+    const int r = route(sendbuf, recvbuf, count == 0, comm, &rc, &kinds);
     if (r < 0) return rc;
     if (!r) return MPIR_intra_collops->Reduce(sendbuf, recvbuf, count, dt, op, root, comm);
     if ((rc = translate(comm, dt, op, &h, &t, &o))) return rc;
+    pass_kinds(h, kinds);
     return mvx_coll_reduce(sendbuf, recvbuf, count, t, o, root, h);
 }
 
 static int mvx_Allreduce(void *sendbuf, void *recvbuf, int count, struct MPIR_DATATYPE *dt,
                          MPI_Op op, struct MPIR_COMMUNICATOR *comm)
 {
-    int h, t, o, rc = MPI_SUCCESS;
-    const int r = route(sendbuf, recvbuf, count == 0, comm, &rc);
+    int h, t, o, rc = MPI_SUCCESS, kinds;
+    const int r = route(sendbuf, recvbuf, count == 0, comm, &rc, &kinds);
     if (r < 0) return rc;
     if (!r) return MPIR_intra_collops->Allreduce(sendbuf, recvbuf, count, dt, op, comm);
     if ((rc = translate(comm, dt, op, &h, &t, &o))) return rc;
+    pass_kinds(h, kinds);
     return mvx_coll_allreduce(sendbuf, recvbuf, count, t, o, h);
 }
 
 static int mvx_Reduce_scatter(void *sendbuf, void *recvbuf, int *recvcnts,
                               struct MPIR_DATATYPE *dt, MPI_Op op, struct MPIR_COMMUNICATOR *comm)
 {
-    int h, t, o, r, rc = MPI_SUCCESS, i, empty = 1;
+    int h, t, o, r, rc = MPI_SUCCESS, i, empty = 1, kinds;
     for (i = 0; i < comm->np && recvcnts; i++) empty &= recvcnts[i] == 0;  /* same counts everywhere */
-    r = route(sendbuf, recvbuf, empty, comm, &rc);
+    r = route(sendbuf, recvbuf, empty, comm, &rc, &kinds);
     if (r < 0) return rc;
     if (!r) return MPIR_intra_collops->Reduce_scatter(sendbuf, recvbuf, recvcnts, dt, op, comm);
     if ((rc = translate(comm, dt, op, &h, &t, &o))) return rc;
+    pass_kinds(h, kinds);
     return mvx_coll_reduce_scatter(sendbuf, recvbuf, recvcnts, t, o, h);
 }
 
 static int mvx_Scan(void *sendbuf, void *recvbuf, int count, struct MPIR_DATATYPE *dt, MPI_Op op,
                     struct MPIR_COMMUNICATOR *comm)
 {
-    int h, t, o, rc = MPI_SUCCESS;
-    const int r = route(sendbuf, recvbuf, count == 0, comm, &rc);
+    int h, t, o, rc = MPI_SUCCESS, kinds;
+    const int r = route(sendbuf, recvbuf, count == 0, comm, &rc, &kinds);
     if (r < 0) return rc;
     if (!r) return MPIR_intra_collops->Scan(sendbuf, recvbuf, count, dt, op, comm);
     if ((rc = translate(comm, dt, op, &h, &t, &o))) return rc;
+    pass_kinds(h, kinds);
     return mvx_coll_scan(sendbuf, recvbuf, count, t, o, h);
 }
 

@@ -138,6 +138,7 @@ def _load():
     c.mvx_comm_set_graphs.argtypes = [i, i]
     c.mvx_comm_last_graph.argtypes = [i, pi, pi]
     c.mvx_comm_graph_stats.argtypes = [i, pi, pi, ctypes.POINTER(ctypes.c_long)]
+    c.mvx_comm_set_call_kinds.argtypes = [i, i]
     c.mvx_comm_reap.argtypes = []
     c.mvx_host_register_enable.argtypes = [i, sz]
     c.mvx_host_unregister.argtypes = [vp]

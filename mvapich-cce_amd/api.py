@@ -175,6 +175,11 @@ class Comm:
         """Capture device calls into HIP graphs and replay them (mvx_comm_set_graphs)."""
         return coll().mvx_comm_set_graphs(self.handle, 1 if on else 0)
 
+    def set_call_kinds(self, kinds):
+        """mvx_comm_set_call_kinds: every rank's buffer kinds in the next
+        blocking call, agreed by the caller (KINDS_UNKNOWN / _DEVICE / _HOST)."""
+        return coll().mvx_comm_set_call_kinds(self.handle, kinds)
+
     def graph_stats(self):
         """{live, retired, destroyed}: graphs held (replayable / kept but never
         replayed) and execs destroyed mid-life (mvx_comm_graph_stats)."""

@@ -23,7 +23,19 @@ typedef struct {
     MPI_Datatype dt;
     MPI_Op op;
     int root;
+    int kinds;            /* every rank's buffer kinds, if agreed (MVX_KINDS_*) */
 } call_t;
+
+/* the hint mvx_comm_set_call_kinds left for this call; consumed by every
+ * call, an early-returning one included */
+static int take_kinds(mvx_comm_t *c)
+{
+    int k;
+    if (!c) return MVX_KINDS_UNKNOWN;
+    k = c->call_kinds;
+    c->call_kinds = MVX_KINDS_UNKNOWN;
+    return k;
+}
 
 /* element counts of rank `rank`'s send / recv vectors */
 static void call_sizes(const call_t *k, int p, int rank, long *nsend, long *nrecv)
@@ -66,7 +78,9 @@ static int run(mvx_comm_t *c, const call_t *k, hipStream_t st, int blocking)
     const int prev = mvxi_dev_enter(c->device);
     int rc;
     if (prev == MVXI_DEV_FAILED) return MPI_ERR_OTHER;
+    c->call_kinds = blocking ? k->kinds : MVX_KINDS_UNKNOWN;
     rc = run_on(c, k, st, blocking);
+    c->call_kinds = MVX_KINDS_UNKNOWN;
     mvxi_dev_leave(c->device, prev);
     return rc;
 }
@@ -149,6 +163,7 @@ int mvx_coll_allreduce(void *sendbuf, void *recvbuf, int count, MPI_Datatype dt,
 {
     mvx_comm_t *c = mvxi_get_comm(comm);
     call_t k;
+    k.kinds = take_kinds(c);
     int rc = MPI_SUCCESS;
     if (!c) return ERR_COMM_NULL_CODE;                       /* TEST_MPI_COMM */
     if (mvx_dtype_info(dt, NULL, NULL)) return ERR_TYPE_NULL_CODE;  /* TEST_DTYPE */
@@ -167,6 +182,7 @@ int mvx_coll_reduce(void *sendbuf, void *recvbuf, int count, MPI_Datatype dt,
 {
     mvx_comm_t *c = mvxi_get_comm(comm);
     call_t k;
+    k.kinds = take_kinds(c);
     int rc = MPI_SUCCESS;
     if (!c) return ERR_COMM_NULL_CODE;
     if (mvx_dtype_info(dt, NULL, NULL)) return ERR_TYPE_NULL_CODE;
@@ -188,6 +204,7 @@ int mvx_coll_reduce_scatter(void *sendbuf, void *recvbuf, int *recvcnts,
 {
     mvx_comm_t *c = mvxi_get_comm(comm);
     call_t k;
+    k.kinds = take_kinds(c);
     int rc = MPI_SUCCESS;
     if (!c) return ERR_COMM_NULL_CODE;
     if (mvx_dtype_info(dt, NULL, NULL)) return ERR_TYPE_NULL_CODE;
@@ -205,6 +222,7 @@ int mvx_coll_scan(void *sendbuf, void *recvbuf, int count, MPI_Datatype dt,
 {
     mvx_comm_t *c = mvxi_get_comm(comm);
     call_t k;
+    k.kinds = take_kinds(c);
     int rc = MPI_SUCCESS;
     if (!c) return ERR_COMM_NULL_CODE;                       /* scan.c:74-80 */
     if (mvx_dtype_info(dt, NULL, NULL)) return ERR_TYPE_NULL_CODE;
@@ -254,6 +272,7 @@ int mvx_allreduce_async(const void *sendbuf, void *recvbuf, int count,
 {
     mvx_comm_t *c = mvxi_get_comm(comm);
     call_t k;
+    k.kinds = take_kinds(c);
     int rc = async_checks(c, dt, op);
     if (rc) return rc;
     if (count < 0) return MPI_ERR_COUNT;
@@ -268,6 +287,7 @@ int mvx_reduce_async(const void *sendbuf, void *recvbuf, int count,
 {
     mvx_comm_t *c = mvxi_get_comm(comm);
     call_t k;
+    k.kinds = take_kinds(c);
     int rc = async_checks(c, dt, op);
     if (rc) return rc;
     if (count < 0) return MPI_ERR_COUNT;
@@ -283,6 +303,7 @@ int mvx_scan_async(const void *sendbuf, void *recvbuf, int count,
 {
     mvx_comm_t *c = mvxi_get_comm(comm);
     call_t k;
+    k.kinds = take_kinds(c);
     int rc = async_checks(c, dt, op);
     if (rc) return rc;
     if (count < 0) return MPI_ERR_COUNT;
@@ -297,6 +318,7 @@ int mvx_reduce_scatter_async(const void *sendbuf, void *recvbuf, const int *recv
 {
     mvx_comm_t *c = mvxi_get_comm(comm);
     call_t k;
+    k.kinds = take_kinds(c);
     int rc = async_checks(c, dt, op);
     if (rc) return rc;
     if (!recvcnts) return MPI_ERR_ARG;

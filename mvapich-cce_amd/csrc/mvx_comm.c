@@ -544,6 +544,15 @@ int mvx_comm_set_host_pipeline(MPI_Comm comm, int on)
     return MPI_SUCCESS;
 }
 
+int mvx_comm_set_call_kinds(MPI_Comm comm, int kinds)
+{
+    mvx_comm_t *c = mvxi_get_comm(comm);
+    if (!c) return ERR_COMM_NULL_CODE;
+    if (kinds < MVX_KINDS_UNKNOWN || kinds > MVX_KINDS_HOST) return MPI_ERR_ARG;
+    c->call_kinds = kinds;
+    return MPI_SUCCESS;
+}
+
 int mvx_comm_set_graphs(MPI_Comm comm, int on)
 {
     mvx_comm_t *c = mvxi_get_comm(comm);

@@ -242,6 +242,7 @@ struct mvx_comm_t {
     int shmem_block;     /* claimed shmem collective block, -1 = none */
     int exch, exch_slices;      /* exchange variant, MVX_EXCH_* (mvx_coll.h) */
     int host_sliced;            /* host buffers at p > 1: sliced pipeline (all ranks' kinds agree) */
+    int call_kinds;             /* the next blocking call's agreed kinds (MVX_KINDS_*), then 0 */
     int has_ops;                /* caller-supplied transport instead of RCCL */
     mvx_transport ops;
     hipStream_t cstream;        /* combine stream of the pipelined exchange */

@@ -514,7 +514,11 @@ int mvxi_typed_copy(mvx_comm_t *c, int dt, long n, const char *send, char *recv,
  * stream) and D2H (another), so both PCIe directions and the collective
  * overlap (run_staged_cs).  The bits are the unsliced plan's (every slice
  * keeps every block boundary).  Stream-ordered calls (mvx_*_async, device
- * buffers by contract) and smaller calls keep the unsliced schedule. */
+ * buffers by contract) and smaller calls keep the unsliced schedule.  A
+ * caller that has agreed every rank's kinds says so per call
+ * (mvx_comm_set_call_kinds): all device -- the unsliced device path, its
+ * exchange variants and graphs; all host -- the sliced pipeline at any
+ * size. */
 static long env_mib(const char *name, long dflt)
 {
     const char *v = getenv(name);
@@ -540,14 +544,19 @@ long mvxi_slice_elems(const mvx_plan *P)
 
 int mvxi_run_job(mvx_comm_t *c, job_t *J, hipStream_t st, int blocking)
 {
-    int rc;
+    int rc, host;
     long cs;
+    const int kinds = blocking ? c->call_kinds : MVX_KINDS_UNKNOWN;
     if (J->P[0].packed) return mvxi_run_job_packed(c, J, st, blocking);
-    if (blocking && J->nr == 1 && !c->local && (cs = mvxi_slice_elems(&J->P[0])) > 0) {
+    if (kinds != MVX_KINDS_UNKNOWN && J->nr == 1) {
+        /* the caller agreed every rank's kinds (mvx_comm_set_call_kinds) */
+        host = mvxi_job_kinds(J);
+        if (host != (kinds == MVX_KINDS_HOST)) return MPI_ERR_BUFFER;
+        if (host) return mvxi_run_staged(c, J, st);     /* every rank slices alike */
+    } else if (blocking && J->nr == 1 && !c->local && (cs = mvxi_slice_elems(&J->P[0])) > 0) {
         mvxi_job_kinds(J);
         return run_staged_cs(c, J, st, cs);
-    }
-    if (mvxi_job_kinds(J)) {
+    } else if (mvxi_job_kinds(J)) {
         if (!blocking) return MPI_ERR_BUFFER;
         if (J->nr == 1 && J->P[0].p > 1 && !c->host_sliced) return run_mirrored(c, J, st);
         return mvxi_run_staged(c, J, st);

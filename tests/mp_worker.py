@@ -276,6 +276,25 @@ def main():
                 case += 1
                 check("scan", dtype, op, (2 << 20) // E + 5, where(), tag="sliced")
                 case += 1
+        # agreed kinds (mvx_comm_set_call_kinds, what the MVAPICH shim passes):
+        # every rank device -> the unsliced device path and its exchange
+        # variant (PIPE here, reported as such); every rank host -> the
+        # sliced pipeline; a hint the buffers contradict -> MPI_ERR_BUFFER on
+        # every rank (all of them contradict it here), before anything moves
+        assert comm.set_exchange(mvx.EXCH_PIPE, 3) == 0
+        for op, dtype in [(102, 10), (111, 17)]:
+            E = mvx.dtype_info(dtype)[0]
+            n = (3 << 20) // E + 7
+            for where, kinds in (("device", mvx.KINDS_DEVICE), ("host", mvx.KINDS_HOST)):
+                assert comm.set_call_kinds(kinds) == 0
+                check("ar", dtype, op, n, where, tag="agreed")
+                report.setdefault("agreed_ran", []).append([where, comm.last_exchange()])
+            s_host = np.zeros(n * E, np.uint8)
+            r_host = np.zeros(n * E, np.uint8)
+            assert comm.set_call_kinds(mvx.KINDS_DEVICE) == 0
+            report.setdefault("contradicted", []).append(
+                mvx.MPI_Allreduce(s_host, r_host, n, dtype, op, comm))
+        assert comm.set_exchange(mvx.EXCH_P2P, 0) == 0
         del os.environ["MVX_SLICE_MIN_MIB"], os.environ["MVX_SLICE_MIB"]
     else:
         # the BASELINE multi-GPU shapes at full size: C3, C4 (p = 4 in the

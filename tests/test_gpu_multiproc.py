@@ -147,9 +147,13 @@ def test_slice_schedule_any_kinds(world, transport):
     all device too; every collective, role-sensitive ops included,
     bit-exact against the oracle's replay."""
     for rep in _launch(world, transport, "sliced", 600):
-        assert rep["checked"] >= 5 * 3 * 5
+        assert rep["checked"] >= 5 * 3 * 5 + 4
         assert not rep["fails"], rep["fails"][:5]
         assert set(rep["ran"]["sliced"]) <= {"0", "-1"}, rep["ran"]     # P2P slices
+        # agreed kinds: all device ran the communicator's variant (PIPE, 1)
+        # unsliced; all host the P2P slices; a contradicted hint -> MPI_ERR_BUFFER
+        assert rep["agreed_ran"] == [["device", 1], ["host", 0]] * 2, rep["agreed_ran"]
+        assert rep["contradicted"] == [1, 1], rep["contradicted"]
 
 
 @pytest.mark.parametrize("world", [2, 4])
