@@ -12,8 +12,15 @@
  *                 bit-exact.  The entries are checked to be gone before the
  *                 second DMA; if they were not, the program stops there.
  *                 The same for mmap'd memory unmapped and mapped again.
+ *   reg_app stress (dry, no GPU): 8 threads at once, each registering and
+ *                 freeing its own mmap'd blocks while others churn small
+ *                 malloc / free and unrelated mmap / munmap: every
+ *                 registration is dropped by its own block's free, exactly
+ *                 once, nothing is left, no thread waits on another for good.
  * Prints "reg_app ok" and one JSON line of what it saw. */
 #define _GNU_SOURCE 1
+#include <malloc.h>
+#include <pthread.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -94,6 +101,53 @@ static int dry(void)
     CHECK(sbrk(-(intptr_t)(2 * MIB)) != (void *)-1 && entries() == 0, "negative sbrk drops");
 
     printf("{\"mode\": \"dry\", \"invalidations\": %ld}\n", mvx_host_register_invalidations() - inv0);
+    return 0;
+}
+
+#define ST_THREADS 8
+#define ST_ITERS 400
+static long st_registered[ST_THREADS], st_failed[ST_THREADS];
+
+static void *st_worker(void *arg)
+{
+    const long t = (long)arg;
+    unsigned seed = 12345u + (unsigned)t;
+    int i, j;
+    for (i = 0; i < ST_ITERS; i++) {
+        size_t n;
+        char *p, *small[8];
+        seed = seed * 1103515245u + 12345u;
+        n = (size_t)(1 + (seed >> 16) % 4) * MIB;          /* 1-4 MiB: mmap'd chunks */
+        p = malloc(n);
+        if (!p) { st_failed[t]++; continue; }
+        p[0] = 1;
+        if (mvx_host_register(p + 64, n - 128) == 0) st_registered[t]++;
+        else st_failed[t]++;
+        for (j = 0; j < 8; j++) small[j] = malloc(32 + 64 * j);   /* the hooks' fast path */
+        if (t % 2) {                                        /* an unrelated mapping */
+            char *m = mmap(NULL, 64 * 1024, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+            if (m != MAP_FAILED) munmap(m, 64 * 1024);
+        }
+        for (j = 0; j < 8; j++) free(small[j]);
+        free(p);
+    }
+    return NULL;
+}
+
+static int stress(void)
+{
+    pthread_t th[ST_THREADS];
+    long t, reg = 0, failed = 0, inv0 = mvx_host_register_invalidations(), inv;
+    mallopt(M_MMAP_THRESHOLD, 512 * 1024);      /* fixed: blocks never share pages */
+    for (t = 0; t < ST_THREADS; t++) CHECK(pthread_create(&th[t], NULL, st_worker, (void *)t) == 0, "thread");
+    for (t = 0; t < ST_THREADS; t++) pthread_join(th[t], NULL);
+    for (t = 0; t < ST_THREADS; t++) { reg += st_registered[t]; failed += st_failed[t]; }
+    inv = mvx_host_register_invalidations() - inv0;
+    printf("{\"mode\": \"stress\", \"threads\": %d, \"registered\": %ld, \"failed\": %ld, \"invalidations\": %ld}\n",
+           ST_THREADS, reg, failed, inv);
+    CHECK(failed == 0, "every registration taken");
+    CHECK(entries() == 0, "nothing left");
+    CHECK(inv == reg, "each registration dropped exactly once, by its own free");
     return 0;
 }
 
@@ -181,7 +235,7 @@ int main(int argc, char **argv)
         printf("FAIL enable\n");
         return 1;
     }
-    rc = !strcmp(argv[1], "dry") ? dry() : !strcmp(argv[1], "gpu") ? gpu() : 2;
+    rc = !strcmp(argv[1], "dry") ? dry() : !strcmp(argv[1], "gpu") ? gpu() : !strcmp(argv[1], "stress") ? stress() : 2;
     mvx_host_register_enable(0, 0);
     if (rc == 0) printf("reg_app ok\n");
     return rc;

@@ -22,7 +22,7 @@ def _reg_app():
     subprocess.check_call(["gcc", "-O2", "-std=gnu99", "-Wall", "-Werror", "-D__HIP_PLATFORM_AMD__",
                            "-I/opt/rocm/include", "-I" + os.path.join(ROOT, "include"),
                            os.path.join(HERE, "reg_app.c"), "-o", out, "-L" + pkg, "-lmvx",
-                           "-L/opt/rocm/lib", "-lamdhip64", "-Wl,-rpath," + pkg, "-Wl,-rpath,/opt/rocm/lib"])
+                           "-L/opt/rocm/lib", "-lamdhip64", "-lpthread", "-Wl,-rpath," + pkg, "-Wl,-rpath,/opt/rocm/lib"])
     return out
 
 
@@ -31,6 +31,16 @@ def test_release_hooks_drop_registrations():
     p = subprocess.run([_reg_app(), "dry"], capture_output=True, text=True, timeout=120, env=env)
     assert p.returncode == 0 and "reg_app ok" in p.stdout, p.stdout[-2000:] + p.stderr[-2000:]
     assert '"invalidations": 7' in p.stdout, p.stdout
+
+
+def test_release_hooks_under_threads():
+    """8 threads register and free their own blocks while others churn small
+    blocks and unrelated mappings: each registration is dropped once, by its
+    own free, and nothing is left (no deadlock: the run is bounded)"""
+    env = dict(os.environ, MVX_HOST_REGISTER_DRY="1")
+    p = subprocess.run([_reg_app(), "stress"], capture_output=True, text=True, timeout=120, env=env)
+    assert p.returncode == 0 and "reg_app ok" in p.stdout, p.stdout[-2000:] + p.stderr[-2000:]
+    assert '"registered": 3200' in p.stdout, p.stdout
 
 
 def test_hooks_inactive_under_ctypes(mvx):
