@@ -65,6 +65,44 @@ __global__ void __launch_bounds__(256) k_t(P8 p)
     if (MODE == 1 && acc.x == 1234.5f) p.d[threadIdx.x] = acc;
 }
 
+// persistent grid, software-pipelined: the loads of the next batch are in
+// flight while the current batch is combined and stored
+template <int U>
+__global__ void __launch_bounds__(256) k_t_pipe(P8 p)
+{
+    __shared__ char lds_cap[56 * 1024];
+    if (p.nvec < 0) lds_cap[threadIdx.x] = 0;
+    const long nthr = (long)gridDim.x * 256;
+    long c0 = (long)blockIdx.x * 256 * U + threadIdx.x;
+    f32x4 cur[U][8], nxt[U][8];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+        if (c0 + u * 256 < p.nvec)
+#pragma unroll
+            for (int q = 0; q < 8; ++q) cur[u][q] = __builtin_nontemporal_load(p.s[q] + c0 + u * 256);
+    for (; c0 < p.nvec; c0 += nthr * U) {
+        const long c1 = c0 + nthr * U;
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (c1 + u * 256 < p.nvec)
+#pragma unroll
+                for (int q = 0; q < 8; ++q) nxt[u][q] = __builtin_nontemporal_load(p.s[q] + c1 + u * 256);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (c0 + u * 256 >= p.nvec) continue;
+#pragma unroll
+            for (int h = 1; h < 8; h <<= 1)
+#pragma unroll
+                for (int q = 0; q + h < 8; q += 2 * h) cur[u][q] = cur[u][q] + cur[u][q + h];
+            __builtin_nontemporal_store(cur[u][0], p.d + c0 + u * 256);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int q = 0; q < 8; ++q) cur[u][q] = nxt[u][q];
+    }
+}
+
 // one 256 MiB stream read (p.s[0] spans all 8 leaves of the set)
 template <int U>
 __global__ void __launch_bounds__(256) k_read1(P8 p)
@@ -83,7 +121,7 @@ __global__ void __launch_bounds__(256) k_read1(P8 p)
 }
 
 typedef void (*KF)(P8);
-struct Var { const char *name; KF f; int U; double moved_leaves; int one_stream; };
+struct Var { const char *name; KF f; int U; double moved_leaves; int one_stream; long grid; };
 
 int main(int argc, char **argv)
 {
@@ -115,8 +153,10 @@ int main(int argc, char **argv)
         {"read8 U2 uncapped", k_t<2, 1, 0, 0>, 2, 8, 0},
         {"write32 U1", k_t<1, 2, 0, 0>, 1, 1, 0},
         {"write32 U2 X8", k_t<2, 2, 0, 8>, 2, 1, 0},
-        {"read1x256 U4", k_read1<4>, 4, 8, 1},
-        {"read1x256 U2", k_read1<2>, 2, 8, 1},
+        {"pipe U1 g512", k_t_pipe<1>, 1, 9, 0, 512},
+        {"pipe U2 g512", k_t_pipe<2>, 2, 9, 0, 512},
+        {"pipe U1 g1024", k_t_pipe<1>, 1, 9, 0, 1024},
+        {"pipe U1 g2048", k_t_pipe<1>, 1, 9, 0, 2048},
     };
     const int NV = sizeof(vars) / sizeof(vars[0]);
     // the tree variants agree with each other on set 0 (0x3c3c3c3c x 8, exact)
@@ -129,7 +169,7 @@ int main(int argc, char **argv)
         for (int v = 0; v < NV; ++v) {
             if (vars[v].moved_leaves != 9) continue;
             CHECK(hipMemset(ps[0].d, 0, leaf));
-            long blocks = ps[0].nvec / (256L * vars[v].U);
+            long blocks = vars[v].grid ? vars[v].grid : ps[0].nvec / (256L * vars[v].U);
             hipLaunchKernelGGL(vars[v].f, dim3(blocks), dim3(256), 0, 0, ps[0]);
             CHECK(hipDeviceSynchronize());
             for (long off : {0L, leaf / 2, leaf - 4096}) {
@@ -147,7 +187,7 @@ int main(int argc, char **argv)
     for (int r = 0; r < rounds; ++r) {
         for (int v = 0; v < NV; ++v) {
             const std::vector<P8> &pp = vars[v].one_stream ? ps1 : ps;
-            const long blocks = (vars[v].one_stream ? pp[0].nvec * 8 : pp[0].nvec) / (256L * vars[v].U);
+            const long blocks = vars[v].grid ? vars[v].grid : (vars[v].one_stream ? pp[0].nvec * 8 : pp[0].nvec) / (256L * vars[v].U);
             for (int w = 0; w < 3; ++w) hipLaunchKernelGGL(vars[v].f, dim3(blocks), dim3(256), 0, 0, pp[w % sets]);
             CHECK(hipEventRecord(e0, 0));
             for (int i = 0; i < 20; ++i) hipLaunchKernelGGL(vars[v].f, dim3(blocks), dim3(256), 0, 0, pp[i % sets]);
