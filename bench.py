@@ -107,6 +107,8 @@ def parse(argv=None):
                          "variant counts as hung (its communicator is aborted and rebuilt)")
     ap.add_argument("--no-native", action="store_true",
                     help="N > 1: skip the RCCL-native reduction timed after the line (SURVEY.md 8(e) ablation)")
+    ap.add_argument("--no-host-e2e", action="store_true",
+                    help="N = 1: skip the host-buffer (PCIe-inclusive) op after the timed region")
     ap.add_argument("--no-kernels", action="store_true",
                     help="N = 1: skip the C3 / C4 / C5 combine-kernel rates after the timed region")
     ap.add_argument("--transport", default="rccl", choices=["rccl", "host", "rccl-net"],
@@ -503,7 +505,9 @@ def run_single(args, mvx, dev, clock):
         out["cpu_baseline"] = cpu_baseline_op(nbytes, args.cpu_seconds)
     if not args.no_kernels:
         out["combine_kernels"] = combine_kernels(mvx)
-    clock.mark("parity, cpu baseline, combine kernels")
+    if not args.no_host_e2e:
+        out["host_end_to_end"] = host_end_to_end(mvx, nbytes)
+    clock.mark("parity, cpu baseline, combine kernels, host end-to-end")
     out["env"] = env_echo()
     out["wall"] = clock.report()
     print(json.dumps(out), flush=True)
@@ -522,6 +526,45 @@ def combine_kernels(mvx):
             BK.run(mvx, "C5", MPI_MAXLOC, MPI_FLOAT_INT, 8, 0, 64 * MIB, 2, quiet=True)]
     return [{k: r[k] for k in ("config", "kernel", "k", "alg_bytes_per_launch", "kernel_us", "hbm_frac")}
             for r in rows]
+
+
+def host_end_to_end(mvx, nbytes, budget=0.25):
+    """After the timed region, never `value`: the same op when the MPI user
+    buffers live in host memory, as the reference's do (north_star: the
+    PCIe-inclusive rate).  MPIR_SUM(invec, inoutvec) on the
+    product's host path -- page-locked operands DMA'd directly, pageable ones
+    through the bounce pipeline -- 2 vectors H2D and 1 D2H per call.  Median
+    call time over `budget` seconds after one checked call (against numpy:
+    float32 sums of small integers are exact)."""
+    import numpy as np
+    import torch
+    n = nbytes // 4
+    rng = np.random.default_rng(7)
+    a = rng.integers(-8, 8, n).astype(np.float32)
+    b = rng.integers(-8, 8, n).astype(np.float32)
+    want = a + b
+    rows = []
+    for where in ("pinned", "pageable"):
+        if where == "pinned":
+            x, y = torch.from_numpy(a).pin_memory(), torch.from_numpy(b).pin_memory()
+        else:
+            x, y = a.copy(), b.copy()
+        mvx.MPIR_call("MPIR_SUM", x, y, n, MPI_FLOAT)
+        got = y.numpy() if torch.is_tensor(y) else y
+        ok = mvx.op_errno() == 0 and bool(np.array_equal(got, want))
+        ts, t_end = [], time.perf_counter() + budget
+        while len(ts) < 3 or time.perf_counter() < t_end:
+            t0 = time.perf_counter()
+            mvx.MPIR_call("MPIR_SUM", x, y, n, MPI_FLOAT)
+            ts.append(time.perf_counter() - t0)
+        ts.sort()
+        t = ts[len(ts) // 2]
+        rows.append({"buffers": where, "ms": round(t * 1e3, 3), "calls": len(ts),
+                     "GiB_per_s_per_vector": round(nbytes / t / GIB, 2),
+                     "pcie_GBps": round(3 * nbytes / t / 1e9, 1), "checked": ok})
+        del x, y
+    return {"op": "MPIR_SUM float32 %d MiB, host operands (2 H2D + 1 D2H per call)" % (nbytes // MIB),
+            "rows": rows}
 
 
 # ------------------------------------------------------------------ common --
