@@ -170,6 +170,23 @@ void mvx_pcopy(void *dst, const void *src, size_t bytes)
     pthread_mutex_unlock(&g_pc_job);
 }
 
+/* How many slices / chunks behind the one just issued a host pipeline drains
+ * its bounced result (MVX_HOST_DRAIN_LAG, 1 or 2; default 2).  Lag 1 (rounds
+ * 1-4) made the host wait for the D2H of the chunk it had just queued the
+ * H2D behind, and the DMA engines idled while it then copied the next chunk
+ * in (tools/drain_lag_ab.sh: pageable 256 MiB op 11.3-13.5 ms against
+ * 12.3-14.2 at lag 1, 64 MiB 3.2-3.3 against 3.5-4.0). */
+int mvxi_host_drain_lag(void)
+{
+    static int lag = 0;
+    if (!lag) {
+        const char *v = getenv("MVX_HOST_DRAIN_LAG");
+        int l = v ? atoi(v) : 2;
+        lag = l < 1 ? 1 : l > STAGE_LAG_MAX ? STAGE_LAG_MAX : l;
+    }
+    return lag;
+}
+
 int mvx_copy_threads(void)
 {
     int n;

@@ -24,16 +24,16 @@ int mvx_op_errno(void)
  * pinned bounce slot by the copy pool (mvx_host.c) and DMA'd from there; a
  * page-locked operand is DMA'd directly.  The kernel runs on stream 0, the
  * D2H of the result on stream 1 (into the bounce, or straight into a
- * page-locked inout), and the host drains chunk c-1 out of the bounce while
- * chunk c is in flight, so host copies, both PCIe directions and the kernel
- * overlap.  Below HOP_BOUNCE_MIN bytes per operand the bounce's per-chunk
+ * page-locked inout), and the host drains chunk c-L out of the bounce after
+ * issuing chunk c, so host copies, both PCIe directions and the kernel
+ * overlap (L: mvxi_host_drain_lag, mvx_host.c).  Below HOP_BOUNCE_MIN bytes per operand the bounce's per-chunk
  * overheads (pool wake-ups, one more copy) cost more than they hide, and
  * pageable operands are handed to HIP's own pageable copy path instead
  * (tools/bench_host.py: 2 MiB 165 vs 299 us, 256 MiB 14.7 vs 12.8 ms;
  * profiles/r02/bench_host.jsonl).  Device operands are used in place; both
  * operands get an HBM mirror (HBM is plentiful, and no device slot is reused
  * while a copy may still read it). */
-#define HOP_NB 3
+#define HOP_NB 4            /* slots: >= the drain lag + 2 (mvxi_host_drain_lag) */
 #define HOP_BOUNCE_MIN (64L << 20)
 #define HOP_CHUNK_MIN (1L << 20)
 #define HOP_CHUNK_MAX (16L << 20)
@@ -70,7 +70,7 @@ static int host_apply_locked(MPI_Op op, MPI_Datatype t, const char *in, char *in
                              int in_dev, int io_dev)
 {
     int e, ts, rc, bounce_in, bounce_io, in_pin, io_pin;
-    long chunk, c, nch;
+    long chunk, c, nch, lag;
     size_t bytes, cb, slot;
     hipStream_t sd;
     mvx_dtype_info(t, &e, &ts);
@@ -107,7 +107,8 @@ static int host_apply_locked(MPI_Op op, MPI_Datatype t, const char *in, char *in
     if ((rc = hop_init(slot, 2 * al256(bytes)))) return rc;
     nch = (len + chunk - 1) / chunk;
     sd = nch > 1 ? g_hop.s[1] : g_hop.s[0];    /* one chunk: everything in order on one stream */
-    for (c = 0; c <= nch; c++) {
+    lag = mvxi_host_drain_lag();
+    for (c = 0; c < nch + lag; c++) {
         if (c < nch) {
             const int b = (int)(c % HOP_NB);
             const long n = len - c * chunk < chunk ? len - c * chunk : chunk;
@@ -138,8 +139,8 @@ static int host_apply_locked(MPI_Op op, MPI_Datatype t, const char *in, char *in
                     return MPI_ERR_OTHER;
             }
         }
-        if (c > 0 && bounce_io) {   /* drain chunk c - 1 */
-            const long p = c - 1;
+        if (c >= lag && bounce_io) {   /* drain chunk c - lag */
+            const long p = c - lag;
             const int b = (int)(p % HOP_NB);
             const long n = len - p * chunk < chunk ? len - p * chunk : chunk;
             if (hipEventSynchronize(g_hop.eout[b]) != hipSuccess) return MPI_ERR_OTHER;

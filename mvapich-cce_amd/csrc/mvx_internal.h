@@ -42,6 +42,7 @@
 #define MVX_BUF_DEVICE   2   /* device or managed memory */
 int mvx_buf_kind(const void *p);   /* one pointer-attribute query */
 int mvx_host_pinned(const void *p);
+int mvxi_host_drain_lag(void);
 void mvx_pcopy(void *dst, const void *src, size_t bytes);
 int mvx_copy_threads(void);
 /* the kind of [p, p + bytes): as mvx_buf_kind, except that with the
@@ -151,7 +152,8 @@ typedef struct {
     char *smir[MVX_MAXP], *rmir[MVX_MAXP], *psend[MVX_MAXP], *precv[MVX_MAXP];
 } packed_bufs_t;
 
-#define STAGE_NB 3
+#define STAGE_NB 4         /* >= the drain lag + 2 (mvxi_host_drain_lag) */
+#define STAGE_LAG_MAX 2
 typedef struct {                  /* a communicator's host-staging resources */
     int ready;
     hipStream_t sh, sd;
@@ -210,7 +212,7 @@ typedef struct mvx_work {
     mvx_plan call_plan;                        /* mvx_api.c run(): this rank's plan */
     mvx_plan pipe[2][MVX_MAXP];                /* PIPE: slice plans, by slice parity */
     rank_exec_t px0[MVX_MAXP], px[2][MVX_MAXP];
-    mvx_plan slice[2][MVX_MAXP];               /* staged: current and previous slice */
+    mvx_plan slice[STAGE_LAG_MAX + 1][MVX_MAXP];   /* staged: the slice being issued and the ones not drained yet */
     job_t pk_job;                              /* packed datatypes */
     packed_bufs_t pk_bufs;
     job_t tc_job;                              /* typed copy */

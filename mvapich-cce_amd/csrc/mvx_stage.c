@@ -29,7 +29,8 @@
 /* ---- host buffers: a sliced pipeline ------------------------------------
  * Slice i of every local rank's plan is staged in (H2D on stream sh), run
  * (phases A-C on the caller's stream), and staged out (D2H on stream sd);
- * the host drains slice i-1 while the device works on slice i, so host
+ * the host drains slice i-L after issuing slice i (L: mvxi_host_drain_lag,
+ * mvx_host.c), so host
  * copies, both PCIe directions and the collective overlap.  Page-locked
  * buffers are moved by DMA directly; pageable ones go through pinned bounce
  * slots filled and emptied by the copy pool (mvx_host.c). */
@@ -179,7 +180,7 @@ static int run_staged_cs(mvx_comm_t *c, const job_t *J, hipStream_t st, long cs_
     stage_job_t S;
     rank_exec_t X[MVX_MAXP];
     size_t need = 0, off[2 * MVX_MAXP], bounce;
-    long span = 0, nsl, i;
+    long span = 0, nsl, i, lag;
     int r, rc, pieces = 0;
     mvx_range v[MVX_MAXP + 1];
 
@@ -243,18 +244,22 @@ static int run_staged_cs(mvx_comm_t *c, const job_t *J, hipStream_t st, long cs_
     if (S.any_host && (rc = stage_init(S.R, bounce))) return rc;
     for (r = 0; r < J->nr; r++) mvxi_plan_slice(&J->P[r], 0, S.cs, &w->slice[0][r]);
     if ((rc = mvxi_job_layout(c, X, J, w->slice[0]))) return rc;   /* slice 0 is the largest */
-    for (i = 0; i < nsl; i++) {
-        mvx_plan *Q = w->slice[i & 1];
-        for (r = 0; r < J->nr; r++) {
-            mvxi_plan_slice(&J->P[r], i, S.cs, &Q[r]);
-            X[r].P = &Q[r];
+    lag = mvxi_host_drain_lag();
+    for (i = 0; i < nsl + lag; i++) {
+        if (i < nsl) {
+            mvx_plan *Q = w->slice[i % (STAGE_LAG_MAX + 1)];
+            for (r = 0; r < J->nr; r++) {
+                mvxi_plan_slice(&J->P[r], i, S.cs, &Q[r]);
+                X[r].P = &Q[r];
+            }
+            if ((rc = stage_in(&S, Q, i, st))) return rc;
+            if ((rc = mvxi_exec_group(X, J->t, J->nr, st, NULL))) return rc;
+            if ((rc = stage_out(&S, Q, i, st))) return rc;
         }
-        if ((rc = stage_in(&S, Q, i, st))) return rc;
-        if ((rc = mvxi_exec_group(X, J->t, J->nr, st, NULL))) return rc;
-        if ((rc = stage_out(&S, Q, i, st))) return rc;
-        if (i > 0 && (rc = stage_drain(&S, w->slice[(i - 1) & 1], i - 1, st))) return rc;
+        if (i >= lag && i - lag < nsl &&
+            (rc = stage_drain(&S, w->slice[(i - lag) % (STAGE_LAG_MAX + 1)], i - lag, st)))
+            return rc;
     }
-    if (nsl > 0 && (rc = stage_drain(&S, w->slice[(nsl - 1) & 1], nsl - 1, st))) return rc;
     return hipStreamSynchronize(st) == hipSuccess ? MPI_SUCCESS : MPI_ERR_OTHER;
 }
 
@@ -306,14 +311,15 @@ static int mirror_in(stage_res_t *R, char *dev, const char *host, size_t bytes, 
 static int mirror_out(stage_res_t *R, char *host, const char *dev, size_t bytes, int kind, hipStream_t st)
 {
     size_t o;
-    long c, nch;
+    long c, nch, lag;
     if (!bytes) return hipStreamSynchronize(st) == hipSuccess ? MPI_SUCCESS : MPI_ERR_OTHER;
     if (!mirror_bounced(kind, bytes)) {
         if (hipMemcpyAsync(host, dev, bytes, hipMemcpyDeviceToHost, st) != hipSuccess) return MPI_ERR_OTHER;
         return hipStreamSynchronize(st) == hipSuccess ? MPI_SUCCESS : MPI_ERR_OTHER;
     }
     nch = (long)((bytes + MIRROR_CHUNK - 1) / MIRROR_CHUNK);
-    for (c = 0; c <= nch; c++) {
+    lag = mvxi_host_drain_lag();
+    for (c = 0; c < nch + lag; c++) {
         if (c < nch) {
             const int b = (int)(c % STAGE_NB);
             o = (size_t)c * MIRROR_CHUNK;
@@ -322,8 +328,8 @@ static int mirror_out(stage_res_t *R, char *host, const char *dev, size_t bytes,
                 hipEventRecord(R->eout[b], st) != hipSuccess)
                 return MPI_ERR_OTHER;
         }
-        if (c > 0) {       /* drain chunk c - 1 while chunk c is in flight */
-            const long p = c - 1;
+        if (c >= lag) {    /* drain chunk c - lag while the later ones are in flight */
+            const long p = c - lag;
             const int b = (int)(p % STAGE_NB);
             o = (size_t)p * MIRROR_CHUNK;
             const size_t n = bytes - o < (size_t)MIRROR_CHUNK ? bytes - o : (size_t)MIRROR_CHUNK;
