@@ -137,9 +137,10 @@ def _back(y, kind):
 @pytest.mark.parametrize("where", ["host-host", "dev-host", "host-dev", "pin-pin", "pin-host", "host-pin",
                                    "dev-pin"])
 def test_mpir_host_buffers(mvx, oracle, n, where):
-    """MPI user buffers live in host memory: the op streams them through HBM
-    (chunked; pageable operands through pinned bounce slots, page-locked ones
-    DMA'd directly; H2D / kernel / D2H overlapped) with the same kernel."""
+    """MPI user buffers live in host memory: pageable operands stream
+    through HBM (chunked, through pinned bounce slots; H2D / kernel / D2H
+    overlapped), page-locked ones are read and written in place by the same
+    kernel when no operand is pageable (zero copy), DMA'd directly otherwise."""
     a, b = T.rand_vec(10, n, 5), T.rand_vec(10, n, 6)
     ref = T.clone(b)
     oracle.op(102, 10, a.view(np.uint8), ref.view(np.uint8), n)
@@ -170,6 +171,43 @@ def test_mpir_host_buffers_types(mvx, oracle, where, dtype, op):
     mvx.MPIR_call(name[op], ia, io, n, dtype)
     assert mvx.op_errno() == 0
     assert np.array_equal(_back(io, ko).view(np.uint8), ref)
+
+
+@pytest.mark.parametrize("shift", [0, 4, 12])
+@pytest.mark.parametrize("dtype,op", [(10, 102), (13, 109), (LDI, 110), (12, 100)])
+def test_mpir_pinned_zero_copy(mvx, oracle, dtype, op, shift):
+    """Page-locked operands on both sides (or one device operand): the op
+    kernel reads and writes them in place over PCIe (csrc/mvx_hostop.c,
+    zero copy).  Interior pointers of pinned allocations, shifted by 0 / 4 /
+    12 bytes against each other's 16-byte alignment (the kernel's element
+    path), ragged counts, bytes outside the vector untouched."""
+    import torch
+    name = {100: "MPIR_MAXF", 102: "MPIR_SUM", 109: "MPIR_BXOR", 110: "MPIR_MINLOC"}
+    E = mvx.dtype_info(dtype)[0]
+    n = (3 << 20) // E + 5
+    a8 = T.rand_vec(dtype, n + 2, 17).view(np.uint8)
+    b8 = T.rand_vec(dtype, n + 2, 18).view(np.uint8)
+    pa = torch.from_numpy(np.concatenate([np.zeros(64, np.uint8), a8])).pin_memory()
+    pb = torch.from_numpy(np.concatenate([np.zeros(64, np.uint8), b8])).pin_memory()
+    before = pb.numpy().copy()
+    ia = pa[64 + E:64 + E + n * E]                        # one element in
+    io = pb[64 + E + shift:64 + E + shift + n * E]        # and shifted
+    ref = io.numpy().copy()
+    oracle.op(op, dtype, ia.numpy().copy(), ref, n)
+    mvx.op_errno()
+    mvx.MPIR_call(name[op], ia, io, n, dtype)
+    assert mvx.op_errno() == 0
+    assert np.array_equal(io.numpy(), ref)
+    whole = pb.numpy()
+    lo, hi = 64 + E + shift, 64 + E + shift + n * E
+    assert np.array_equal(whole[:lo], before[:lo]) and np.array_equal(whole[hi:], before[hi:])
+    # device `in`, page-locked `inout`
+    io2 = torch.from_numpy(b8[:n * E].copy()).pin_memory()
+    ref2 = io2.numpy().copy()
+    oracle.op(op, dtype, a8[:n * E].copy(), ref2, n)
+    mvx.MPIR_call(name[op], T.to_dev(a8[:n * E]), io2, n, dtype)
+    assert mvx.op_errno() == 0
+    assert np.array_equal(io2.numpy(), ref2)
 
 
 def test_special_values_float(mvx, oracle):
