@@ -505,6 +505,7 @@ def run_single(args, mvx, dev, clock):
         out["cpu_baseline"] = cpu_baseline_op(nbytes, args.cpu_seconds)
     if not args.no_kernels:
         out["combine_kernels"] = combine_kernels(mvx)
+        roof["mix_ceiling"] = mix_ceiling(x_in, x_io, nbytes, achieved, stream)
     if not args.no_host_e2e:
         out["host_end_to_end"] = host_end_to_end(mvx, nbytes)
     clock.mark("parity, cpu baseline, combine kernels, host end-to-end")
@@ -526,6 +527,46 @@ def combine_kernels(mvx):
             BK.run(mvx, "C5", MPI_MAXLOC, MPI_FLOAT_INT, 8, 0, 64 * MIB, 2, quiet=True)]
     return [{k: r[k] for k in ("config", "kernel", "k", "alg_bytes_per_launch", "kernel_us", "hbm_frac")}
             for r in rows]
+
+
+def mix_ceiling(x_in, x_io, nbytes, achieved_gbs, stream, reps=20):
+    """After the timed region: what this GPU's HBM reaches for the C2
+    kernel's own traffic on the same rotating buffers -- both vectors read
+    alone, one written alone, a copy (tools/ceiling.hip, the fastest form of
+    each stream in tools/tune_sum3.hip).  Two ceilings for the 2-read /
+    1-write kernel: `additive` -- the reads' time plus the write's, as if
+    reads and writes never shared the bus (a bound no mixed stream was seen
+    to reach: the copy kernel makes 0.91 of it); `mixed_line` -- the rate on
+    the line from read-only (write share 0) to copy (1/2) at the kernel's
+    write share 1/3.  8 TB/s stays the line's `peak`."""
+    import ctypes
+    path = os.path.join(ROOT, "tools", "libmvx_ceiling.so")
+    try:
+        lib = ctypes.CDLL(path)
+    except OSError as e:
+        return {"error": "%s: %s" % (os.path.relpath(path, ROOT), e)}
+    fn = lib.mvx_ceiling_run
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p), ctypes.c_int,
+                   ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_float)]
+    sets = len(x_in)
+    a = (ctypes.c_void_p * sets)(*[t.data_ptr() for t in x_in])
+    b = (ctypes.c_void_p * sets)(*[t.data_ptr() for t in x_io])
+    us = {}
+    for mode, name in ((0, "read2"), (1, "write1"), (2, "copy")):
+        t = ctypes.c_float()
+        if fn(mode, a, b, sets, nbytes, reps, ctypes.c_void_p(stream.cuda_stream), ctypes.byref(t)):
+            return {"error": "mvx_ceiling_run(%d) failed" % mode}
+        us[name] = float(t.value)
+    read_gbs = 2 * nbytes / (us["read2"] * 1e-6) / 1e9
+    copy_gbs = 2 * nbytes / (us["copy"] * 1e-6) / 1e9
+    additive = 3 * nbytes / ((us["read2"] + us["write1"]) * 1e-6) / 1e9
+    line = read_gbs + (copy_gbs - read_gbs) * (1 / 3) / (1 / 2)
+    return {"read_GBs": round(read_gbs, 1), "write_GBs": round(nbytes / (us["write1"] * 1e-6) / 1e9, 1),
+            "copy_GBs": round(copy_gbs, 1), "us": {k: round(v, 2) for k, v in us.items()},
+            "additive_GBs": round(additive, 1), "frac_of_additive": round(achieved_gbs / additive, 4),
+            "mixed_line_GBs": round(line, 1), "frac_of_mixed_line": round(achieved_gbs / line, 4),
+            "note": "measured ceilings of the kernel's own 2-read/1-write mix (tools/ceiling.hip); not the peak"}
 
 
 def host_end_to_end(mvx, nbytes, budget=0.25):
