@@ -72,7 +72,10 @@ static int hop_init(size_t slot, size_t dev)
  * included: tools/zc_attr.hip).  256 MiB SUM float32 9.94-10.07 ms against
  * 10.9 ms for 2 H2D + kernel + 1 D2H through HBM (tools/zc_probe.hip: a
  * kernel's PCIe reads reach 55 GB/s, the DMA engines' 57.5).
- * MVX_HOST_ZEROCOPY=0 keeps the DMA pipeline for them. */
+ * MVX_HOST_ZEROCOPY=0 keeps the DMA pipeline for them.  Pageable operands
+ * keep the DMA pipeline: a kernel reading the pinned bounce slots in place
+ * (just filled by the copy pool) ran the 256 MiB op in 13.8-14.4 ms against
+ * 11.4-11.5 through HBM (tools/zc_ab.sh, profiles/r05/zero_copy_bounce_ab.jsonl). */
 static int zerocopy_on(void)
 {
     static int on = -1;
