@@ -107,8 +107,10 @@ def parse(argv=None):
                          "variant counts as hung (its communicator is aborted and rebuilt)")
     ap.add_argument("--no-native", action="store_true",
                     help="N > 1: skip the RCCL-native reduction timed after the line (SURVEY.md 8(e) ablation)")
-    ap.add_argument("--no-host-e2e", action="store_true",
-                    help="N = 1: skip the host-buffer (PCIe-inclusive) op after the timed region")
+    ap.add_argument("--host-e2e", action="store_true",
+                    help="N = 1: also time the op on host buffers (PCIe-inclusive) after the timed region; "
+                         "off by default: it launches the measured kernel template on PCIe-bound operands, "
+                         "which would skew a kernel-trace average of the same command")
     ap.add_argument("--no-kernels", action="store_true",
                     help="N = 1: skip the C3 / C4 / C5 combine-kernel rates after the timed region")
     ap.add_argument("--transport", default="rccl", choices=["rccl", "host", "rccl-net"],
@@ -506,7 +508,7 @@ def run_single(args, mvx, dev, clock):
     if not args.no_kernels:
         out["combine_kernels"] = combine_kernels(mvx)
         roof["mix_ceiling"] = mix_ceiling(x_in, x_io, nbytes, achieved, stream)
-    if not args.no_host_e2e:
+    if args.host_e2e:
         out["host_end_to_end"] = host_end_to_end(mvx, nbytes)
     clock.mark("parity, cpu baseline, combine kernels, host end-to-end")
     out["env"] = env_echo()
