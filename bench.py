@@ -560,10 +560,17 @@ def mix_ceiling(x_in, x_io, nbytes, achieved_gbs, stream, reps=20):
         if fn(mode, a, b, sets, nbytes, reps, ctypes.c_void_p(stream.cuda_stream), ctypes.byref(t)):
             return {"error": "mvx_ceiling_run(%d) failed" % mode}
         us[name] = float(t.value)
+    return ceiling_summary(nbytes, us, achieved_gbs)
+
+
+def ceiling_summary(nbytes, us, achieved_gbs):
+    """The two ceilings of a 2-read / 1-write stream of `nbytes` vectors from
+    the launch times (us) of reading both vectors ("read2"), writing one
+    ("write1") and copying one ("copy"); see mix_ceiling."""
     read_gbs = 2 * nbytes / (us["read2"] * 1e-6) / 1e9
     copy_gbs = 2 * nbytes / (us["copy"] * 1e-6) / 1e9
     additive = 3 * nbytes / ((us["read2"] + us["write1"]) * 1e-6) / 1e9
-    line = read_gbs + (copy_gbs - read_gbs) * (1 / 3) / (1 / 2)
+    line = read_gbs + (copy_gbs - read_gbs) * (1 / 3) / (1 / 2)   # write share 1/3 on the 0 .. 1/2 line
     return {"read_GBs": round(read_gbs, 1), "write_GBs": round(nbytes / (us["write1"] * 1e-6) / 1e9, 1),
             "copy_GBs": round(copy_gbs, 1), "us": {k: round(v, 2) for k, v in us.items()},
             "additive_GBs": round(additive, 1), "frac_of_additive": round(achieved_gbs / additive, 4),

@@ -187,3 +187,19 @@ def test_launcher_counts_gpus_without_torch(tmp_path, monkeypatch):
     assert started == ["0", "1"]
     started.clear()
     assert bench.launch(args, 3, ["--gpus", "3"]) == 2 and started == []
+
+
+def test_mix_ceiling_summary():
+    """bench.ceiling_summary: the additive bound is 3 vectors over the
+    read-both plus write-one times; the mixed line sits two thirds of the way
+    from the read-only rate to the copy rate (write share 1/3 of 1/2)."""
+    sys.path.insert(0, ROOT)
+    import bench
+    nb = 1 << 28
+    us = {"read2": 80.0, "write1": 40.0, "copy": 90.0}
+    d = bench.ceiling_summary(nb, us, 6400.0)
+    read, copy = 2 * nb / 80e-6 / 1e9, 2 * nb / 90e-6 / 1e9
+    assert abs(d["additive_GBs"] - 3 * nb / 120e-6 / 1e9) < 0.1
+    assert abs(d["mixed_line_GBs"] - (read + (copy - read) * 2 / 3)) < 0.1
+    assert d["frac_of_additive"] == round(6400.0 / (3 * nb / 120e-6 / 1e9), 4)
+    assert copy < d["mixed_line_GBs"] < read
