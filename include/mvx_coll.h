@@ -302,9 +302,12 @@ typedef struct mvx_collops {
 extern const mvx_collops MVX_device_collops;
 
 /* ---- predefined ops as MPI_User_functions (global_ops.c) ---------------
- * invec / inoutvec may be device or host memory (host operands are streamed
- * through HBM in 32 MiB chunks, H2D / kernel / D2H overlapped); the call
- * completes before it returns.  An undefined (op, type) pair leaves the data alone and sets
+ * invec / inoutvec may be device or host memory: when neither is pageable
+ * (device, or page-locked: hipHostMalloc'd, hipHostRegister'ed, or pinned by
+ * the registration cache) the kernel reads and writes them in place
+ * (MVX_HOST_ZEROCOPY=0: through HBM instead); pageable operands are streamed
+ * through HBM in chunks, H2D / kernel / D2H overlapped.  The call completes
+ * before it returns.  An undefined (op, type) pair leaves the data alone and sets
  * mvx_op_errno() to 329, as MPIR_Op_errno (global_ops.c:41). */
 void MPIR_MAXF(void *, void *, int *, MPI_Datatype *);
 void MPIR_MINF(void *, void *, int *, MPI_Datatype *);
