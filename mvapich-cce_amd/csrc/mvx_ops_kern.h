@@ -248,6 +248,82 @@ template <typename T> struct CG {
 template <typename T> struct Chunk {
     T e[CG<T>::v];
 };
+// 1-byte elements stay in their four 32-bit words (the SWAR chunk op, CF8):
+// as 16 byte members the loads and stores were split into bytes and packed
+// again around every op
+template <> struct Chunk<uint8_t> { uint32_t w[4]; };
+template <> struct Chunk<int8_t> { uint32_t w[4]; };
+
+// The op over a whole chunk, a = op(a, b) element by element.  One-byte
+// types run as SWAR on the chunk's four 32-bit words: element by element
+// the compiler extracted, combined and re-packed every byte, and the 1-byte
+// apply kernels ran at 0.65-0.73 of HBM peak against 0.78-0.81 for every
+// wider type (tools/bench_kernels.py all, profiles/r05/bench_kernels_all.jsonl).
+template <int O, typename T>
+struct CF {
+    static __device__ __forceinline__ void f(Chunk<T> &a, const Chunk<T> &b)
+    {
+#pragma unroll
+        for (int j = 0; j < CG<T>::v; ++j) a.e[j] = F<O, T>::f(a.e[j], b.e[j]);
+    }
+};
+
+typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));   // one packed-16 register
+
+// per byte of a word: 0x80 if the byte is nonzero, else 0
+__device__ __forceinline__ uint32_t swar_nz(uint32_t x)
+{
+    return (((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x) & 0x80808080u;
+}
+
+// bytes as two packed-16 lanes each (even bytes, odd bytes), op lane-wise,
+// low 8 bits of each lane kept: unsigned MAX / MIN, wrapping PROD
+template <int O>
+__device__ __forceinline__ uint32_t swar_p16(uint32_t a, uint32_t b)
+{
+    const uint32_t ae = a & 0x00ff00ffu, ao = (a >> 8) & 0x00ff00ffu;
+    const uint32_t be = b & 0x00ff00ffu, bo = (b >> 8) & 0x00ff00ffu;
+    u16x2 xe, xo, ye, yo, re, ro;
+    __builtin_memcpy(&xe, &ae, 4); __builtin_memcpy(&xo, &ao, 4);
+    __builtin_memcpy(&ye, &be, 4); __builtin_memcpy(&yo, &bo, 4);
+    if constexpr (O == OMAX) { re = __builtin_elementwise_max(xe, ye); ro = __builtin_elementwise_max(xo, yo); }
+    else if constexpr (O == OMIN) { re = __builtin_elementwise_min(xe, ye); ro = __builtin_elementwise_min(xo, yo); }
+    else { re = xe * ye; ro = xo * yo; }
+    uint32_t e, o;
+    __builtin_memcpy(&e, &re, 4); __builtin_memcpy(&o, &ro, 4);
+    return (e & 0x00ff00ffu) | ((o & 0x00ff00ffu) << 8);
+}
+
+// one word of four 1-byte elements, op O; SIGNED: int8_t MAX / MIN
+template <int O, bool SIGNED>
+__device__ __forceinline__ uint32_t swar8(uint32_t a, uint32_t b)
+{
+    if constexpr (O == OBAND) return a & b;
+    else if constexpr (O == OBOR) return a | b;
+    else if constexpr (O == OBXOR) return a ^ b;
+    else if constexpr (O == OSUM) return ((a & 0x7f7f7f7fu) + (b & 0x7f7f7f7fu)) ^ ((a ^ b) & 0x80808080u);
+    else if constexpr (O == OLAND) return (swar_nz(a) & swar_nz(b)) >> 7;
+    else if constexpr (O == OLOR) return (swar_nz(a) | swar_nz(b)) >> 7;
+    else if constexpr (O == OLXOR) return (swar_nz(a) ^ swar_nz(b)) >> 7;
+    else if constexpr (SIGNED) return swar_p16<O>(a ^ 0x80808080u, b ^ 0x80808080u) ^ 0x80808080u;   // biased order
+    else return swar_p16<O>(a, b);
+}
+
+template <int O, bool SIGNED>
+struct CF8 {
+    template <typename T>
+    static __device__ __forceinline__ void f(Chunk<T> &a, const Chunk<T> &b)
+    {
+#pragma unroll
+        for (int w = 0; w < 4; ++w) a.w[w] = swar8<O, SIGNED>(a.w[w], b.w[w]);
+    }
+};
+template <int O> struct CF<O, uint8_t> {
+    static __device__ __forceinline__ void f(Chunk<uint8_t> &a, const Chunk<uint8_t> &b) { CF8<O, false>::f(a, b); }
+};
+template <int O> struct CF<O, int8_t> {
+    static __device__ __forceinline__ void f(Chunk<int8_t> &a, const Chunk<int8_t> &b) { CF8<O, true>::f(a, b); }
+};
 
 // whole-element store: the pair padding is an explicit member carried from
 // leaf 0, so the element path writes the same bytes as the 16-byte path
@@ -403,8 +479,7 @@ k_combine(const Params P)
                     const long c = c0 + (long)u * 256;
                     if (c < P.nvec) {
                         const Chunk<T> f = ld_chunk<T, NT>(fold[q], c);
-#pragma unroll
-                        for (int j = 0; j < V; ++j) x[u][q].e[j] = F<O, T>::f(x[u][q].e[j], f.e[j]);
+                        CF<O, T>::f(x[u][q], f);
                     }
                 }
             }
@@ -416,8 +491,7 @@ k_combine(const Params P)
             if (k == 2) {
 #pragma unroll
                 for (int u = 0; u < U; ++u)
-#pragma unroll
-                    for (int j = 0; j < V; ++j) x[u][0].e[j] = F<O, T>::f(x[u][0].e[j], x[u][1].e[j]);
+                    CF<O, T>::f(x[u][0], x[u][1]);
             }
         } else if constexpr (PROG == 1) {
 #pragma unroll
@@ -426,8 +500,7 @@ k_combine(const Params P)
                 for (int q = 0; q + h < KMAX; q += 2 * h)
 #pragma unroll
                     for (int u = 0; u < U; ++u)
-#pragma unroll
-                        for (int j = 0; j < V; ++j) x[u][q].e[j] = F<O, T>::f(x[u][q].e[j], x[u][q + h].e[j]);
+                        CF<O, T>::f(x[u][q], x[u][q + h]);
         } else {
 #pragma unroll
             for (int l = 0; (1 << l) < KMAX; ++l) {
@@ -436,9 +509,7 @@ k_combine(const Params P)
                     if (tmask & (1u << (l * 8 + q))) {
 #pragma unroll
                         for (int u = 0; u < U; ++u)
-#pragma unroll
-                            for (int j = 0; j < V; ++j)
-                                x[u][q].e[j] = F<O, T>::f(x[u][q].e[j], x[u][q + (1 << l)].e[j]);
+                            CF<O, T>::f(x[u][q], x[u][q + (1 << l)]);
                     }
                 }
             }
@@ -447,8 +518,7 @@ k_combine(const Params P)
                 if (cmask & (1u << q)) {
 #pragma unroll
                     for (int u = 0; u < U; ++u)
-#pragma unroll
-                        for (int j = 0; j < V; ++j) x[u][0].e[j] = F<O, T>::f(x[u][0].e[j], x[u][q].e[j]);
+                        CF<O, T>::f(x[u][0], x[u][q]);
                 }
             }
         }
@@ -491,7 +561,6 @@ k_tree_body(const BodyParams P)
 {
     __shared__ char lds_cap[BODY_LDS_CAP];
     if (P.nvec < 0) lds_cap[threadIdx.x] = 0;
-    constexpr int V = CG<T>::v;
     const long nthr = (long)gridDim.x * 256;
     for (long c0 = (long)blockIdx.x * (256 * U) + threadIdx.x; c0 < P.nvec; c0 += nthr * U) {
         Chunk<T> x[U][KMAX];
@@ -510,8 +579,7 @@ k_tree_body(const BodyParams P)
                 for (int h = 1; h < KMAX; h <<= 1)
 #pragma unroll
                     for (int q = 0; q + h < KMAX; q += 2 * h)
-#pragma unroll
-                        for (int j = 0; j < V; ++j) x[u][q].e[j] = F<O, T>::f(x[u][q].e[j], x[u][q + h].e[j]);
+                        CF<O, T>::f(x[u][q], x[u][q + h]);
                 st_chunk<T, BODY_ST_NT>(P.dst, c, x[u][0]);
             }
         }
@@ -526,7 +594,6 @@ k_chain_body(const BodyParams P)
 {
     __shared__ char lds_cap[BODY_LDS_CAP];
     if (P.nvec < 0) lds_cap[threadIdx.x] = 0;
-    constexpr int V = CG<T>::v;
     const long nthr = (long)gridDim.x * 256;
     for (long c0 = (long)blockIdx.x * (256 * U) + threadIdx.x; c0 < P.nvec; c0 += nthr * U) {
         Chunk<T> x[U][KMAX];
@@ -543,8 +610,7 @@ k_chain_body(const BodyParams P)
             if (c < P.nvec) {
 #pragma unroll
                 for (int q = 1; q < KMAX; ++q)
-#pragma unroll
-                    for (int j = 0; j < V; ++j) x[u][0].e[j] = F<O, T>::f(x[u][0].e[j], x[u][q].e[j]);
+                    CF<O, T>::f(x[u][0], x[u][q]);
                 st_chunk<T, BODY_ST_NT>(P.dst, c, x[u][0]);
             }
         }
@@ -789,6 +855,17 @@ static KSet kset(const char *name)
 {
     KSet s;
     s.apply = kfam<O, T, 2, 4, 4, 0>(FAM_APPLY);
+    if constexpr (std::is_same<T, pxi>::value && (O == OMAXLOC || O == OMINLOC)) {
+        // the plain op on MPI_LONG_DOUBLE_INT as lane pairs too (the trees'
+        // k_pxi_loc_body with KMAX = 2): one 32-byte element per lane ran it
+        // at 0.56 of HBM peak (profiles/r05/bench_kernels_all.jsonl)
+        s.apply.body = (const void *)&k_pxi_loc_body<O, 2, 1>;
+        s.apply.body_sym = &ksym_pxi_body<O, 2, 1>;
+        s.apply.body_unroll = 1;
+        s.apply.body_k = 2;
+        s.apply.body_units = 2;
+        s.apply.body_cap = env_int("MVX_PXI_APPLY_CAP", 4);
+    }
     // (a 2-leaf body at U = 3 and 2 blocks per CU ran 123.8 vs 126.4 us in
     // the standalone sweep, profiles/r02/tune_occ_k2.jsonl, but 124.8 vs
     // 123.5-124.8 us in the product: not adopted)

@@ -104,3 +104,51 @@ def test_long_double_int_loc_pair_body(mvx, op, k):
     sym, got, ref = _run(mvx, op, 22, k, SHAPE_TREE, n, offset=8, seed=2)
     assert sym.startswith("k_combine<"), sym
     assert np.array_equal(got, ref)
+
+
+@pytest.mark.parametrize("op", [110, 111])
+def test_long_double_int_loc_pair_apply(mvx, oracle, op):
+    """The plain op (MPIR_MAXLOC / MINLOC, k = 2) on MPI_LONG_DOUBLE_INT runs
+    the lane-pair body too when large and aligned (k_pxi_loc_body<O, 2, 1>):
+    bit for bit against the oracle's x87, 30 % tied values (the loc = min
+    rule), in place on inout; misaligned operands run k_combine."""
+    import torch
+    n = 1 << 20                          # 32 MiB per operand: a non-temporal launch
+    for seed, off in ((3, 0), (4, 16), (5, 8)):
+        a, b = T.rand_vec(22, n, 300 + seed), T.rand_vec(22, n, 400 + seed)
+        rng = np.random.default_rng(seed)
+        sel = rng.random(n) < 0.3
+        a.view(np.uint8).reshape(n, -1)[sel, :10] = b.view(np.uint8).reshape(n, -1)[sel, :10]
+        ref = T.clone(b)
+        oracle.op(op, 22, a.view(np.uint8), ref.view(np.uint8), n)
+        buf_a = torch.zeros(n * 32 + 64, dtype=torch.uint8, device="cuda")
+        buf_b = torch.zeros(n * 32 + 64, dtype=torch.uint8, device="cuda")
+        da, db = buf_a[off:off + n * 32], buf_b[off:off + n * 32]
+        da.copy_(torch.from_numpy(a.view(np.uint8).copy()))
+        db.copy_(torch.from_numpy(b.view(np.uint8).copy()))
+        assert mvx.op_apply(op, 22, da, db, n) == 0
+        torch.cuda.synchronize()
+        sym = mvx.last_kernel_symbol()
+        # 16-byte aligned (offset 0 or 16): the pair body; offset 8: no whole
+        # element starts on the 16-byte grid, the element path
+        assert sym.startswith("k_pxi_loc_body<%d, 2, " % (11 if op == 111 else 10)) if off % 16 == 0 else \
+            sym.startswith("k_combine<"), sym
+        assert np.array_equal(db.cpu().numpy(), ref.view(np.uint8))
+
+
+@pytest.mark.parametrize("k", [2, 4, 8])
+@pytest.mark.parametrize("shape", [SHAPE_TREE, SHAPE_CHAIN])
+@pytest.mark.parametrize("op,dtype", [(102, 1), (103, 2), (100, 1), (101, 1), (100, 2), (101, 2), (104, 1),
+                                      (106, 2), (108, 1), (105, 3), (107, 3), (109, 3)])
+def test_one_byte_types_swar(mvx, op, dtype, k, shape):
+    """1-byte elements run the SWAR chunk op (four bytes per 32-bit word:
+    wrapping SUM / PROD, signed and unsigned MAX / MIN, the logical ops'
+    0 / 1 bytes, the bitwise ops) in every kernel family -- the plain op,
+    the masked program, the tree and chain bodies -- bit for bit against the
+    oracle, at a non-temporal size and at a small one with head / tail
+    elements around the 16-byte body."""
+    E = mvx.dtype_info(dtype)[0]
+    assert E == 1
+    for n, off in ((NT_ELEMS * 4 + 3, 0), (4099, 5)):
+        sym, got, ref = _run(mvx, op, dtype, k, shape, n, offset=off, seed=k)
+        assert np.array_equal(got, ref), (sym, n)
