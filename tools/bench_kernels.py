@@ -104,7 +104,7 @@ def main():
             run(mvx, "C3-leaf%dMiB" % mib, mvx.MPI_SUM, mvx.MPI_FLOAT, 8, 0, mib * MIB, 4 if mib <= 64 else 2)
         for mib in (32, 128, 256):
             run(mvx, "C5-leaf%dMiB" % mib, mvx.MPI_MAXLOC, mvx.MPI_FLOAT_INT, 8, 0, mib * MIB, 4 if mib <= 64 else 2)
-    if "all" in sys.argv[1:]:
+    if "all" in sys.argv[1:] and "all-tree" not in sys.argv[1:]:
         # every defined (op, type) pair's apply kernel at 256 MiB vectors
         # (the op functions' and a 2-leaf combine's kernel): the whole op
         # table against the HBM peak, one line each
@@ -116,6 +116,16 @@ def main():
                 if hip.mvx_op_supported(op, t) != 1:
                     continue
                 run(mvx, "A-%d-%d" % (op, t), op, t, 2, 1, 256 * MIB, 4, reps=10, warm=2)
+    if "all-tree" in sys.argv[1:]:
+        # the same pairs as 8-leaf trees over 32 MiB leaves (the C3 shape)
+        hip = mvx.hip()
+        types = [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 17, 18, 19, 20, 21, 22, 23, 24,
+                 25, 26, 27, 28, 29, 30, 31, 32, 33]
+        for op in range(100, 112):
+            for t in types:
+                if hip.mvx_op_supported(op, t) != 1:
+                    continue
+                run(mvx, "T-%d-%d" % (op, t), op, t, 8, 0, 32 * MIB, 4, reps=10, warm=2)
     if "x87" in sys.argv[1:]:
         # x87 long double (integer emulation): apply and the C3 / C5 shapes
         run(mvx, "X2-sum", mvx.MPI_SUM, mvx.MPI_LONG_DOUBLE, 2, 1, 256 * MIB, 4)
