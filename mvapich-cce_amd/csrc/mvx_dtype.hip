@@ -50,6 +50,11 @@ struct Type {
     // the map on the device, split into pieces of <= 64 bytes
     void *dmap;
     long dmap_n;
+    // the map as W-byte units (W = 16, 8, 4: index 0, 1, 2): each unit's
+    // offset in the element, in packed order; 0: not built; -1: the map
+    // does not split into W-byte units
+    int *dunits[3];
+    long units[3];
 };
 
 static Type g_t[MVX_TYPE_DERIVED_MAX];
@@ -65,6 +70,8 @@ static Type *slot(int h)
 static void reset(Type &t)
 {
     if (t.dmap) (void)hipFree(t.dmap);
+    for (int w = 0; w < 3; ++w)
+        if (t.dunits[w]) (void)hipFree(t.dunits[w]);
     t = Type();
 }
 
@@ -529,6 +536,97 @@ k_pack(const char *__restrict__ src, char *__restrict__ dst, const DBlk *__restr
     }
 }
 
+// Units of W bytes (tools/bench_pack.py: the piece kernel above reached
+// 0.25-0.39 of HBM peak on every shape, 64 KiB of the packed stream per
+// wave spread over 64 pieces and a 64-bit division per piece).  Lane l of
+// the grid takes packed units l, l + T, l + 2T, ... (T the grid's threads):
+// one wave reads or writes 64 consecutive units of the packed stream, and on
+// the extent side the units of one block are consecutive too.  The unit's
+// (element, unit-in-element) pair advances by the grid stride's (D, R) with
+// no division after the first; U units per lane are in flight at once.
+typedef uint32_t pu32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t pu32x4 __attribute__((ext_vector_type(4)));
+template <int W> struct UnitT;
+template <> struct UnitT<4> { typedef uint32_t t; };
+template <> struct UnitT<8> { typedef pu32x2 t; };
+template <> struct UnitT<16> { typedef pu32x4 t; };
+
+template <bool PACK, int W, int U>
+__global__ void __launch_bounds__(256)
+k_pack_units(const char *__restrict__ src, char *__restrict__ dst, const int *__restrict__ uoff, long upe,
+             long count, long extent, long D, long R)
+{
+    typedef typename UnitT<W>::t V;
+    const long T = (long)gridDim.x * 256;
+    const long N = count * upe;
+    long q = (long)blockIdx.x * 256 + threadIdx.x;
+    long i = q / upe, j = q - i * upe;
+    while (q < N) {
+        V v[U];
+        char *to[U];
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            to[k] = nullptr;
+            if (q < N) {
+                const long e = i * extent + uoff[j];
+                const char *from = PACK ? src + e : src + q * W;
+                to[k] = PACK ? dst + q * W : dst + e;
+                v[k] = __builtin_nontemporal_load((const V *)from);
+            }
+            q += T;
+            i += D;
+            j += R;
+            if (j >= upe) { j -= upe; ++i; }
+        }
+#pragma unroll
+        for (int k = 0; k < U; ++k)
+            if (to[k]) __builtin_nontemporal_store(v[k], (V *)to[k]);
+    }
+}
+
+// the unit table for W (index wi), built once per type; false if the map
+// does not split into W-byte units
+static bool unit_table(Type &t, int W, int wi)
+{
+    if (t.units[wi] < 0) return false;
+    if (t.dunits[wi]) return true;
+    std::vector<int> u;
+    bool ok = t.extent > 0 && t.extent % W == 0 && t.size % W == 0 && t.size / W <= (1L << 22);
+    for (size_t b = 0; ok && b < t.map.size(); ++b) {
+        const Blk &m = t.map[b];
+        if (((m.off % W) + W) % W || m.len % W || m.off < INT32_MIN || m.off + m.len > INT32_MAX) { ok = false; break; }
+        for (long o = 0; o < m.len; o += W) u.push_back((int)(m.off + o));
+    }
+    if (!ok || u.empty()) { t.units[wi] = -1; return false; }
+    if (hipMalloc(&t.dunits[wi], u.size() * sizeof(int)) != hipSuccess) {
+        t.dunits[wi] = nullptr;
+        t.units[wi] = -1;
+        return false;
+    }
+    if (hipMemcpy(t.dunits[wi], u.data(), u.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess) {
+        (void)hipFree(t.dunits[wi]);
+        t.dunits[wi] = nullptr;
+        t.units[wi] = -1;
+        return false;
+    }
+    t.units[wi] = (long)u.size();
+    return true;
+}
+
+template <bool PACK, int W>
+static int launch_units(const Type &t, int wi, const void *src, void *dst, long count, hipStream_t st)
+{
+    constexpr int U = 4;
+    const long upe = t.units[wi], N = count * upe;
+    long blocks = (N + 256L * U - 1) / (256L * U);
+    if (blocks > 65536) blocks = 65536;
+    if (blocks < 1) blocks = 1;
+    const long T = blocks * 256;
+    hipLaunchKernelGGL((k_pack_units<PACK, W, U>), dim3((unsigned)blocks), dim3(256), 0, st, (const char *)src,
+                       (char *)dst, (const int *)t.dunits[wi], upe, count, t.extent, T / upe, T % upe);
+    return hipGetLastError() == hipSuccess ? MPI_SUCCESS : MPI_ERR_OTHER;
+}
+
 static int device_map(Type &t)
 {
     if (t.dmap) return MPI_SUCCESS;
@@ -562,6 +660,25 @@ static int pack(int h, const void *src, void *dst, size_t count, hipStream_t st,
         return MPI_ERR_TYPE;   // the padded pair structs move whole (mvx_dtype.h dense)
     }
     if (!count || !t->size) return MPI_SUCCESS;
+    {
+        static int units_on = -1;    // MVX_PACK_UNITS=0: the piece kernel only (A/B)
+        if (units_on < 0) {
+            const char *e = getenv("MVX_PACK_UNITS");
+            units_on = e ? atoi(e) != 0 : 1;
+        }
+        const uintptr_t al = (uintptr_t)src | (uintptr_t)dst;
+        const int Ws[3] = {16, 8, 4};
+        for (int wi = 0; units_on && wi < 3; ++wi) {
+            const int W = Ws[wi];
+            if (al % W || !unit_table(*t, W, wi)) continue;
+            if (W == 16) return packing ? launch_units<true, 16>(*t, wi, src, dst, (long)count, st)
+                                        : launch_units<false, 16>(*t, wi, src, dst, (long)count, st);
+            if (W == 8) return packing ? launch_units<true, 8>(*t, wi, src, dst, (long)count, st)
+                                       : launch_units<false, 8>(*t, wi, src, dst, (long)count, st);
+            return packing ? launch_units<true, 4>(*t, wi, src, dst, (long)count, st)
+                           : launch_units<false, 4>(*t, wi, src, dst, (long)count, st);
+        }
+    }
     int rc = device_map(*t);
     if (rc) return rc;
     const long items = (long)count * t->dmap_n;
