@@ -551,16 +551,25 @@ template <> struct UnitT<4> { typedef uint32_t t; };
 template <> struct UnitT<8> { typedef pu32x2 t; };
 template <> struct UnitT<16> { typedef pu32x4 t; };
 
-template <bool PACK, int W, int U>
+#define UNITS_LDS 2048   // unit tables this small are read from LDS
+
+template <bool PACK, int W, int U, bool LDS>
 __global__ void __launch_bounds__(256)
 k_pack_units(const char *__restrict__ src, char *__restrict__ dst, const int *__restrict__ uoff, long upe,
              long count, long extent, long D, long R)
 {
     typedef typename UnitT<W>::t V;
+    __shared__ int s_uoff[LDS ? UNITS_LDS : 1];
+    if constexpr (LDS) {
+        for (int u = threadIdx.x; u < (int)upe; u += 256) s_uoff[u] = uoff[u];
+        __syncthreads();
+    }
     const long T = (long)gridDim.x * 256;
     const long N = count * upe;
+    const long DX = D * extent;                   // the element offset's advance per grid stride
     long q = (long)blockIdx.x * 256 + threadIdx.x;
     long i = q / upe, j = q - i * upe;
+    long ix = i * extent;                         // i * extent, carried
     while (q < N) {
         V v[U];
         char *to[U];
@@ -568,15 +577,15 @@ k_pack_units(const char *__restrict__ src, char *__restrict__ dst, const int *__
         for (int k = 0; k < U; ++k) {
             to[k] = nullptr;
             if (q < N) {
-                const long e = i * extent + uoff[j];
+                const long e = ix + (LDS ? s_uoff[j] : uoff[j]);
                 const char *from = PACK ? src + e : src + q * W;
                 to[k] = PACK ? dst + q * W : dst + e;
                 v[k] = __builtin_nontemporal_load((const V *)from);
             }
             q += T;
-            i += D;
+            ix += DX;
             j += R;
-            if (j >= upe) { j -= upe; ++i; }
+            if (j >= upe) { j -= upe; ix += extent; }
         }
 #pragma unroll
         for (int k = 0; k < U; ++k)
@@ -622,8 +631,14 @@ static int launch_units(const Type &t, int wi, const void *src, void *dst, long 
     if (blocks > 65536) blocks = 65536;
     if (blocks < 1) blocks = 1;
     const long T = blocks * 256;
-    hipLaunchKernelGGL((k_pack_units<PACK, W, U>), dim3((unsigned)blocks), dim3(256), 0, st, (const char *)src,
-                       (char *)dst, (const int *)t.dunits[wi], upe, count, t.extent, T / upe, T % upe);
+    if (upe <= UNITS_LDS)
+        hipLaunchKernelGGL((k_pack_units<PACK, W, U, true>), dim3((unsigned)blocks), dim3(256), 0, st,
+                           (const char *)src, (char *)dst, (const int *)t.dunits[wi], upe, count, t.extent, T / upe,
+                           T % upe);
+    else
+        hipLaunchKernelGGL((k_pack_units<PACK, W, U, false>), dim3((unsigned)blocks), dim3(256), 0, st,
+                           (const char *)src, (char *)dst, (const int *)t.dunits[wi], upe, count, t.extent, T / upe,
+                           T % upe);
     return hipGetLastError() == hipSuccess ? MPI_SUCCESS : MPI_ERR_OTHER;
 }
 
