@@ -126,6 +126,14 @@ def main():
                 if hip.mvx_op_supported(op, t) != 1:
                     continue
                 run(mvx, "T-%d-%d" % (op, t), op, t, 8, 0, 32 * MIB, 4, reps=10, warm=2)
+    if "ks" in sys.argv[1:]:
+        # every leaf count 2..8, tree and chain (the masked program where no
+        # body kernel fits: k = 3, 5, 6, 7), f32 SUM and int64 BAND, 32 MiB leaves
+        for op, t in ((mvx.MPI_SUM, mvx.MPI_FLOAT), (mvx.MPI_BAND, mvx.MPI_LONG)):
+            for shape in (0, 1):
+                for k in range(2, 9):
+                    run(mvx, "K-%d-%d-%s-k%d" % (op, t, "tree" if shape == 0 else "chain", k), op, t, k, shape,
+                        32 * MIB, 4, reps=10, warm=2)
     if "x87" in sys.argv[1:]:
         # x87 long double (integer emulation): apply and the C3 / C5 shapes
         run(mvx, "X2-sum", mvx.MPI_SUM, mvx.MPI_LONG_DOUBLE, 2, 1, 256 * MIB, 4)
