@@ -125,6 +125,7 @@ static int g_block_cap = 1 << 20;
 // Non-temporal above this many bytes touched by one launch (all operands +
 // the result); below it the result is likely re-read from L2 / MALL.
 static long g_nt_min_bytes = 64L << 20;
+static int g_prog4 = 1;          // programs over 3-4 leaves on the KMAX = 4 kernels
 static int g_prog_u = 1;
 static int g_generic_only = 0;   // MVX_PROG_GENERIC=1: no fixed-tree kernels (A/B runs)
 // resident blocks per CU for the non-temporal launches of each family (0 =
@@ -184,6 +185,8 @@ static void init_env()
     if (e && atoi(e) == 2) g_prog_u = 2;
     e = getenv("MVX_PROG_GENERIC");
     if (e && atoi(e) == 1) g_generic_only = 1;
+    e = getenv("MVX_PROG4");
+    if (e && atoi(e) == 0) g_prog4 = 0;
     e = getenv("MVX_NO_BODY");
     if (e && atoi(e) == 1) g_no_body = 1;
     const char *caps[FAM_N] = {"MVX_CAP_APPLY", "MVX_CAP_PROG", "MVX_CAP_TREE"};
@@ -333,6 +336,8 @@ extern "C" int mvx_op_program(int op, int dtype, const void *const *srcs,
         return launch(ks, k == 8 ? ks->chain8 : ks->chain4, P, (hipStream_t)stream);
     if (g_prog_u == 2 && ks->prog2.fn[0])
         return launch(ks, ks->prog2, P, (hipStream_t)stream);
+    if (k <= 4 && g_prog4)
+        return launch(ks, ks->prog4, P, (hipStream_t)stream);
     return launch(ks, ks->prog, P, (hipStream_t)stream);
 }
 

@@ -766,6 +766,7 @@ struct KSet {
     KFam apply;            // KMAX 2 (k <= 2)
     KFam prog;             // KMAX 8 combine program (masks)
     KFam prog2;            // 4-byte types: the U = 2 program (MVX_PROG_U=2); fn[0] null otherwise
+    KFam prog4;            // programs over 3 or 4 leaves: KMAX 4 at U = 2 (MVX_PROG4=0: prog)
     KFam tree8, tree4;     // PROG = 1: full trees over 8 / 4 leaves
     KFam chain8, chain4;   // full chains over 8 / 4 leaves: k_chain_body, else the masked program
     int esize;
@@ -882,6 +883,11 @@ static KSet kset(const char *name)
     }
     s.chain8 = kchain<O, T, 8>();
     s.chain4 = kchain<O, T, 4>();
+    if constexpr (alu_heavy<T>::v) {
+        s.prog4 = kfam<O, T, 4, 1, 1, 0>(FAM_PROG);
+    } else {
+        s.prog4 = kfam<O, T, 4, 2, 2, 0>(FAM_PROG);
+    }
     if constexpr (sizeof(T) == 4) {
         s.prog2 = kfam<O, T, MVX_COMBINE_KMAX, 2, 2, 0>(FAM_PROG);
     } else {
