@@ -510,7 +510,7 @@ def run_single(args, mvx, dev, clock):
         roof["mix_ceiling"] = mix_ceiling(x_in, x_io, nbytes, achieved, stream)
     if args.host_e2e:
         out["host_end_to_end"] = host_end_to_end(mvx, nbytes)
-    clock.mark("parity, cpu baseline, combine kernels, host end-to-end")
+    clock.mark("parity, cpu baseline, combine kernels, ceilings")
     out["env"] = env_echo()
     out["wall"] = clock.report()
     print(json.dumps(out), flush=True)
