@@ -152,3 +152,20 @@ def test_one_byte_types_swar(mvx, op, dtype, k, shape):
     for n, off in ((NT_ELEMS * 4 + 3, 0), (4099, 5)):
         sym, got, ref = _run(mvx, op, dtype, k, shape, n, offset=off, seed=k)
         assert np.array_equal(got, ref), (sym, n)
+
+
+@pytest.mark.parametrize("shape", [SHAPE_TREE, SHAPE_CHAIN])
+@pytest.mark.parametrize("folded", [False, True])
+@pytest.mark.parametrize("op,dtype", [(102, 10), (105, 8), (111, 17)])
+def test_three_leaf_programs_on_four_leaf_kernel(mvx, op, dtype, shape, folded):
+    """Programs over three leaves (and four with folded leaves) run the
+    4-leaf program kernel at U = 2 (KSet::prog4), non-temporal size: the
+    launched template names KMAX 4, and the bits are the oracle's."""
+    E = mvx.dtype_info(dtype)[0]
+    n = NT_ELEMS * 4 // E
+    for k in (3, 4):
+        if k == 4 and not folded:
+            continue                      # the plain 4-leaf tree / chain runs its body kernel
+        sym, got, ref = _run(mvx, op, dtype, k, shape, n, folded=folded)
+        assert sym.startswith("k_combine<") and ", 4, 2, 1, 0>" in sym, sym
+        assert np.array_equal(got, ref)
