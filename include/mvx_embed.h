@@ -90,15 +90,23 @@ int mvx_host_hooks_active(void);
 /* Registers [addr, addr + bytes) now (as a call using it would): 0, or
  * MPI_ERR_OTHER (cache off, range below the minimum, refused). */
 int mvx_host_register(const void *addr, size_t bytes);
-/* Drops every registration containing addr: 0, or MPI_ERR_ARG if none. */
+/* Drops every registration containing addr: 0, or MPI_ERR_ARG if none.  A
+ * registration a call in flight is using is unregistered when that call is
+ * done. */
 int mvx_host_unregister(const void *addr);
 /* Drops every registration overlapping [addr, addr + bytes), which is about
  * to be released (the reference's find_and_free_dregs_inside, dreg.c:1063):
- * the number dropped. */
+ * the number dropped.  Safe to call from inside a memory hook: it makes no
+ * HIP call -- the registrations leave the cache at once and are unregistered
+ * at the next libmvx entry, after the last call using them (dreg.c:678-767). */
 int mvx_host_invalidate(const void *addr, size_t bytes);
 int mvx_host_register_stats(long *entries, size_t *bytes, long *hits, long *misses);
 /* registrations dropped by releases (hooks and mvx_host_invalidate) so far */
 long mvx_host_register_invalidations(void);
+/* dropped registrations not unregistered yet, registrations held by calls in
+ * flight, and hipHostUnregister calls made so far (in dry mode: that would
+ * have been made) */
+int mvx_host_register_deferred(long *deferred, long *held, long *unregisters);
 
 /* The buffer kinds of every rank in the next blocking collective call on
  * `comm`, when the caller has agreed them across ranks (the MVAPICH shim
@@ -107,8 +115,10 @@ long mvx_host_register_invalidations(void);
  * variants; MVX_KINDS_HOST -- every rank passes host memory: host calls of
  * any size overlap their copies in slices; MVX_KINDS_UNKNOWN (the default,
  * also "mixed") -- the schedule that pairs with any kind.
- * Every rank must pass the same value; the next call consumes it.  A call
- * whose own buffers contradict the hint returns MPI_ERR_BUFFER (1). */
+ * Every rank must pass the same value; the next call consumes it.  Every
+ * rank runs the schedule the hint names, so a rank whose own buffers
+ * contradict it still pairs with its peers (host buffers under DEVICE go
+ * through HBM mirrors; device buffers under HOST are used in place). */
 #define MVX_KINDS_UNKNOWN 0
 #define MVX_KINDS_DEVICE 1
 #define MVX_KINDS_HOST 2

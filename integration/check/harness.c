@@ -14,7 +14,9 @@
  * (the shim's route and creation agreements, counted apart from the data
  * calls) move their bytes through a board in a file every rank maps, with a
  * time limit so a rank that never arrives fails the call instead of hanging
- * the test. */
+ * the test.  The route agreement's ints are kept for the test to read
+ * (h_last_route), and a CPU test may declare ranges device memory
+ * (h_fake_device: the build routes the shim's device test here). */
 #include <stdlib.h>
 #include <string.h>
 #include <fcntl.h>
@@ -25,6 +27,11 @@
 #include "mpiimpl.h"
 #include "mpiops.h"
 #include "mpicoll.h"
+
+/* the build renames the shim's device test to h_buffer_is_device (Makefile);
+ * libmvx's own test under its real name */
+#undef mvx_buffer_is_device
+int mvx_buffer_is_device(const void *p);
 
 extern MPIR_COLLOPS MPIR_mvx_collops;
 void MPIR_mvx_collops_init(void);
@@ -176,20 +183,68 @@ static int agreement(int n, struct MPIR_DATATYPE *d, MPI_Op op)
     return d->self == MPI_INT && n >= 1 && n <= 4 && (op == MPI_MAX || op == MPI_MIN);
 }
 
+/* the last route agreement (three ints): this rank's and the reduced ones */
+static int g_route_n, g_route_mine[4], g_route_all[4];
+
 static int host_agree(const int *s, int *r, int n, MPI_Op op, struct MPIR_COMMUNICATOR *c)
 {
     int all[BOARD_RANKS * 4], i, q;
     g_agree_calls++;
-    if (c->np == 1) { memcpy(r, s, (size_t)n * sizeof(int)); return MPI_SUCCESS; }
-    if (board_allgather(s, n * (int)sizeof(int), all)) return MPI_ERR_OTHER;
-    for (i = 0; i < n; i++) {
-        r[i] = all[i];
-        for (q = 1; q < c->np; q++) {
-            const int v = all[q * n + i];
-            if (op == MPI_MAX ? v > r[i] : v < r[i]) r[i] = v;
+    if (c->np == 1) {
+        memcpy(r, s, (size_t)n * sizeof(int));
+    } else {
+        if (board_allgather(s, n * (int)sizeof(int), all)) return MPI_ERR_OTHER;
+        for (i = 0; i < n; i++) {
+            r[i] = all[i];
+            for (q = 1; q < c->np; q++) {
+                const int v = all[q * n + i];
+                if (op == MPI_MAX ? v > r[i] : v < r[i]) r[i] = v;
+            }
         }
     }
+    if (n == 3) {
+        g_route_n++;
+        memcpy(g_route_mine, s, 3 * sizeof(int));
+        memcpy(g_route_all, r, 3 * sizeof(int));
+    }
     return MPI_SUCCESS;
+}
+
+/* the last route agreement's ints (mine[3], all[3]); returns how many route
+ * agreements there have been */
+int h_last_route(int *mine, int *all)
+{
+    memcpy(mine, g_route_mine, 3 * sizeof(int));
+    memcpy(all, g_route_all, 3 * sizeof(int));
+    return g_route_n;
+}
+
+/* ---- buffer kinds ------------------------------------------------------- */
+/* ranges a CPU test declares device memory (no GPU here); anything else is
+ * what libmvx says */
+#define NFAKE 16
+static struct { const char *p; long n; } g_fake[NFAKE];
+
+int h_fake_device(const void *p, long bytes)
+{
+    int i;
+    for (i = 0; i < NFAKE; i++)
+        if (!g_fake[i].p) {
+            g_fake[i].p = (const char *)p;
+            g_fake[i].n = bytes;
+            return 0;
+        }
+    return 1;
+}
+
+void h_fake_device_clear(void) { memset(g_fake, 0, sizeof g_fake); }
+
+int h_buffer_is_device(const void *p)
+{
+    int i;
+    for (i = 0; i < NFAKE; i++)
+        if (g_fake[i].p && (const char *)p >= g_fake[i].p && (const char *)p < g_fake[i].p + g_fake[i].n) return 1;
+    return mvx_buffer_is_device(p);
 }
 static int host_reduce(void *s, void *r, int n, struct MPIR_DATATYPE *d, MPI_Op op, int root,
                     struct MPIR_COMMUNICATOR *c)

@@ -34,20 +34,28 @@
  * ranks run the same function (comm_util.c:321-331 installs one table per
  * communicator; intra_fns_new.c:5453), so the choice between libmvx and
  * MVAPICH's own function is agreed, never taken rank-locally:
- *   MVX_SHIM_ROUTE=agree (default)  one MPIR_intra_collops->Allreduce of two
- *                 ints (MPI_MAX of {device buffers here, host buffers here})
- *                 on the host path: if any rank passes device memory (or sets
- *                 MVX_HOST_BUFFERS=1) every rank calls libmvx -- a host-buffer
- *                 rank through libmvx's host staging -- otherwise every rank
- *                 runs MVAPICH's function.  Skipped at np == 1 and for an
- *                 empty call (count 0 on every rank, as MPI requires).
+ *   MVX_SHIM_ROUTE=agree (default)  one MPIR_intra_collops->Allreduce of three
+ *                 ints (MPI_MAX of {this rank touches device memory, this
+ *                 rank touches host memory, this rank's translation error})
+ *                 on the host path: if any rank touches device memory (or
+ *                 sets MVX_HOST_BUFFERS=1) every rank calls libmvx -- a
+ *                 host-buffer rank through libmvx's host staging -- otherwise
+ *                 every rank runs MVAPICH's function.  "Touches" counts only
+ *                 the buffers the call uses on that rank: sendbuf when it
+ *                 holds elements, recvbuf unless the rank is a non-root of
+ *                 Reduce (or receives no element of a Reduce_scatter).  Skipped
+ *                 at np == 1 and for an empty call (count 0 on every rank, as
+ *                 MPI requires).
  *   MVX_SHIM_ROUTE=local   no agreement: the caller promises every rank's
  *                 buffers agree in kind in every call (the route is this
  *                 rank's own buffer test).
  *   MVX_SHIM_ROUTE must be the same on every rank, like any MVAPICH knob.
- *   The agreement also tells libmvx when every rank passes device memory
+ *   The agreement also tells libmvx when no rank touches host memory
  *   (mvx_comm_set_call_kinds): large calls then keep the unsliced device
- *   schedule instead of the slices that pair with host-buffer ranks.
+ *   schedule instead of the slices that pair with host-buffer ranks.  One
+ *   rank's device sendbuf beside its host recvbuf counts as host.
+ *   The datatype and op are translated before the agreement (below), so a
+ *   rank that cannot translate makes every rank return its error.
  *
  * Translation, per call, cached:
  *   communicator  the first call routed to libmvx creates the twin, on every
@@ -63,7 +71,8 @@
  *                 every later call routed to libmvx returns MPI_ERR_OTHER on
  *                 every rank.  device = $MVX_DEVICE_ID, else the
  *                 MPI_COMM_WORLD rank modulo the visible GPUs.
- *   datatype      a permanent type's handle is libmvx's handle (the values
+ *   datatype      (local, before the route agreement; cached)
+ *                 a permanent type's handle is libmvx's handle (the values
  *                 of include/mpi.h:64-140); a derived type is rebuilt from
  *                 the node tree the reference's constructors stored
  *                 (type_contig.c:118-169, type_hvec.c:98-160,
@@ -74,7 +83,8 @@
  *                 the reference's or the call fails with MPI_ERR_TYPE.  User
  *                 functions are given the caller's handle
  *                 (mvx_type_set_handle).
- *   op            predefined ops pass unchanged; a user op
+ *   op            (local, before the route agreement)
+ *                 predefined ops pass unchanged; a user op
  *                 (!permanent) is registered once with mvx_op_create.
  *   flavour       _SMP_ builds pass the live knobs (enable_shmem_collectives,
  *                 the VIADEV_* thresholds, comm->shmem_coll_ok) so libmvx
@@ -403,104 +413,141 @@ int mvx_shim_op(MPI_Op op, int *out)
 
 /* ---- the collops members ------------------------------------------------ */
 
-/* this rank's wish: 1 for libmvx (device memory, or MVX_HOST_BUFFERS=1) */
-static int wants_mvx(const void *sendbuf, const void *recvbuf)
-{
-    const char *e = getenv("MVX_HOST_BUFFERS");
-    if (e && atoi(e) == 1) return 1;
-    return mvx_buffer_is_device(sendbuf) || mvx_buffer_is_device(recvbuf);
-}
-
 static int route_local(void)
 {
     const char *e = getenv("MVX_SHIM_ROUTE");
     return e && !strcmp(e, "local");
 }
 
-/* The route of one call, the same on every rank: 1 libmvx, 0 MVAPICH's own
- * function; `empty` (no element on any rank) needs no agreement.  A failed
- * agreement returns -1 with *rc set.  *kinds: what the agreement learnt of
- * every rank's buffers (MVX_KINDS_*), for libmvx's choice of schedule. */
-static int route(const void *sendbuf, const void *recvbuf, int empty, struct MPIR_COMMUNICATOR *comm,
-                 int *rc, int *kinds)
+/* What one call does with this rank's buffers: the buffers it touches here
+ * (libmvx's own rule, mvx_api.c call_sizes: sendbuf when it holds elements;
+ * recvbuf when this rank receives -- never at a non-root of Reduce, whose
+ * recvbuf MPI leaves unspecified) and whether any of them is host memory. */
+typedef struct {
+    const void *sendbuf, *recvbuf;
+    int send_used, recv_used;
+    int empty;          /* no element on any rank (the same on every rank) */
+} shim_call;
+
+static int touches_device(const shim_call *k)
 {
-    int v[2], all[2];
-    const int dev = mvx_buffer_is_device(sendbuf) || mvx_buffer_is_device(recvbuf);
-    const int mine = wants_mvx(sendbuf, recvbuf);
+    return (k->send_used && mvx_buffer_is_device(k->sendbuf)) ||
+           (k->recv_used && mvx_buffer_is_device(k->recvbuf));
+}
+
+static int touches_host(const shim_call *k)
+{
+    return (k->send_used && !mvx_buffer_is_device(k->sendbuf)) ||
+           (k->recv_used && !mvx_buffer_is_device(k->recvbuf));
+}
+
+/* this rank's wish: 1 for libmvx (a device buffer, or MVX_HOST_BUFFERS=1) */
+static int wants_mvx(const shim_call *k)
+{
+    const char *e = getenv("MVX_HOST_BUFFERS");
+    if (e && atoi(e) == 1) return 1;
+    return touches_device(k);
+}
+
+/* The route of one call, the same on every rank: 1 libmvx (*t, *o: the
+ * datatype and op in libmvx's handles), 0 MVAPICH's own function, -1 with
+ * *rc set: every rank returns *rc.  An empty call needs no agreement.
+ *
+ * A call that may go to libmvx is translated first -- locally, cached -- so
+ * that the one agreement also carries whether every rank could: a rank whose
+ * derived type does not rebuild to the reference's bounds, or whose user op
+ * cannot be registered, makes every rank return its error instead of leaving
+ * its peers inside RCCL.  The agreement is one MPI_MAX Allreduce of three
+ * ints: {this rank wants libmvx, this rank touches host memory, this rank's
+ * translation error}.  *kinds: MVX_KINDS_DEVICE when no rank touches host
+ * memory (libmvx then keeps the unsliced device schedule for large calls),
+ * else MVX_KINDS_UNKNOWN (the schedule that pairs with every kind). */
+static int route(const shim_call *k, struct MPIR_DATATYPE *dt, MPI_Op op, struct MPIR_COMMUNICATOR *comm,
+                 int *t, int *o, int *rc, int *kinds)
+{
+    int v[3], all[3], trc;
+    const int mine = wants_mvx(k), local = comm->np == 1 || route_local();
     *kinds = MVX_KINDS_UNKNOWN;
-    if (empty || comm->np == 1 || route_local()) return mine && !empty;
+    *rc = MPI_SUCCESS;
+    if (k->empty || (local && !mine)) return 0;
+    trc = mvx_shim_type(dt, t);
+    if (trc == MPI_SUCCESS) trc = mvx_shim_op(op, o);
+    if (local) {
+        *rc = trc;
+        return trc ? -1 : 1;
+    }
     v[0] = mine;
-    v[1] = !dev;
-    *rc = MPIR_intra_collops->Allreduce(v, all, 2, MPIR_GET_DTYPE_PTR(MPI_INT), MPI_MAX, comm);
+    v[1] = touches_host(k);
+    v[2] = trc;
+    *rc = MPIR_intra_collops->Allreduce(v, all, 3, MPIR_GET_DTYPE_PTR(MPI_INT), MPI_MAX, comm);
     if (*rc != MPI_SUCCESS) return -1;
-    /* all[1]: some rank's buffers are host memory */
-    *kinds = !all[1] ? MVX_KINDS_DEVICE : MVX_KINDS_UNKNOWN;
-    return all[0] != 0;
+    if (!all[0]) return 0;
+    if (all[2]) {           /* some rank cannot translate: every rank fails alike */
+        *rc = all[2];
+        return -1;
+    }
+    *kinds = all[1] ? MVX_KINDS_UNKNOWN : MVX_KINDS_DEVICE;
+    return 1;
 }
 
-/* hand the agreed kinds to libmvx for the call about to be made on h */
-static void pass_kinds(int h, int kinds)
+/* the communicator's twin (collective at first use: every rank is here, the
+ * route being agreed) with the agreed kinds handed over for the call about
+ * to be made on it; -1 if the twin could not be created */
+static int twin_for_call(struct MPIR_COMMUNICATOR *comm, int kinds)
 {
-    if (kinds != MVX_KINDS_UNKNOWN) mvx_comm_set_call_kinds(h, kinds);
-}
-
-/* communicator, datatype and op in libmvx's handles */
-static int translate(struct MPIR_COMMUNICATOR *comm, struct MPIR_DATATYPE *dt, MPI_Op op,
-                     int *h, int *t, int *o)
-{
-    int rc;
-    /* the communicator first: its creation is collective, the rest local */
-    if ((*h = shim_comm(comm)) < 0) return MPI_ERR_OTHER;
-    if ((rc = mvx_shim_type(dt, t))) return rc;
-    return mvx_shim_op(op, o);
+    const int h = shim_comm(comm);
+    if (h >= 0 && kinds != MVX_KINDS_UNKNOWN) mvx_comm_set_call_kinds(h, kinds);
+    return h;
 }
 
 static int mvx_Reduce(void *sendbuf, void *recvbuf, int count, struct MPIR_DATATYPE *dt, MPI_Op op,
                       int root, struct MPIR_COMMUNICATOR *comm)
 {
-    int h, t, o, rc = MPI_SUCCESS, kinds;
-    const int r = route(sendbuf, recvbuf, count == 0, comm, &rc, &kinds);
+    const shim_call k = {sendbuf, recvbuf, count > 0, count > 0 && comm->local_rank == root, count == 0};
+    int h, t, o, rc, kinds;
+    const int r = route(&k, dt, op, comm, &t, &o, &rc, &kinds);
     if (r < 0) return rc;
     if (!r) return MPIR_intra_collops->Reduce(sendbuf, recvbuf, count, dt, op, root, comm);
-    if ((rc = translate(comm, dt, op, &h, &t, &o))) return rc;
-    pass_kinds(h, kinds);
+    if ((h = twin_for_call(comm, kinds)) < 0) return MPI_ERR_OTHER;
     return mvx_coll_reduce(sendbuf, recvbuf, count, t, o, root, h);
 }
 
 static int mvx_Allreduce(void *sendbuf, void *recvbuf, int count, struct MPIR_DATATYPE *dt,
                          MPI_Op op, struct MPIR_COMMUNICATOR *comm)
 {
-    int h, t, o, rc = MPI_SUCCESS, kinds;
-    const int r = route(sendbuf, recvbuf, count == 0, comm, &rc, &kinds);
+    const shim_call k = {sendbuf, recvbuf, count > 0, count > 0, count == 0};
+    int h, t, o, rc, kinds;
+    const int r = route(&k, dt, op, comm, &t, &o, &rc, &kinds);
     if (r < 0) return rc;
     if (!r) return MPIR_intra_collops->Allreduce(sendbuf, recvbuf, count, dt, op, comm);
-    if ((rc = translate(comm, dt, op, &h, &t, &o))) return rc;
-    pass_kinds(h, kinds);
+    if ((h = twin_for_call(comm, kinds)) < 0) return MPI_ERR_OTHER;
     return mvx_coll_allreduce(sendbuf, recvbuf, count, t, o, h);
 }
 
 static int mvx_Reduce_scatter(void *sendbuf, void *recvbuf, int *recvcnts,
                               struct MPIR_DATATYPE *dt, MPI_Op op, struct MPIR_COMMUNICATOR *comm)
 {
-    int h, t, o, r, rc = MPI_SUCCESS, i, empty = 1, kinds;
-    for (i = 0; i < comm->np && recvcnts; i++) empty &= recvcnts[i] == 0;  /* same counts everywhere */
-    r = route(sendbuf, recvbuf, empty, comm, &rc, &kinds);
+    shim_call k = {sendbuf, recvbuf, 0, 0, 1};
+    int h, t, o, r, rc, i, kinds;
+    for (i = 0; i < comm->np && recvcnts; i++) k.send_used |= recvcnts[i] > 0;  /* same counts everywhere */
+    k.empty = !k.send_used;
+    k.recv_used = recvcnts && recvcnts[comm->local_rank] > 0;
+    r = route(&k, dt, op, comm, &t, &o, &rc, &kinds);
     if (r < 0) return rc;
     if (!r) return MPIR_intra_collops->Reduce_scatter(sendbuf, recvbuf, recvcnts, dt, op, comm);
-    if ((rc = translate(comm, dt, op, &h, &t, &o))) return rc;
-    pass_kinds(h, kinds);
+    if ((h = twin_for_call(comm, kinds)) < 0) return MPI_ERR_OTHER;
     return mvx_coll_reduce_scatter(sendbuf, recvbuf, recvcnts, t, o, h);
 }
 
 static int mvx_Scan(void *sendbuf, void *recvbuf, int count, struct MPIR_DATATYPE *dt, MPI_Op op,
                     struct MPIR_COMMUNICATOR *comm)
 {
-    int h, t, o, rc = MPI_SUCCESS, kinds;
-    const int r = route(sendbuf, recvbuf, count == 0, comm, &rc, &kinds);
+    const shim_call k = {sendbuf, recvbuf, count > 0, count > 0, count == 0};
+    int h, t, o, rc, kinds;
+    const int r = route(&k, dt, op, comm, &t, &o, &rc, &kinds);
     if (r < 0) return rc;
     if (!r) return MPIR_intra_collops->Scan(sendbuf, recvbuf, count, dt, op, comm);
-    if ((rc = translate(comm, dt, op, &h, &t, &o))) return rc;
-    pass_kinds(h, kinds);
+    if ((h = twin_for_call(comm, kinds)) < 0) return MPI_ERR_OTHER;
     return mvx_coll_scan(sendbuf, recvbuf, count, t, o, h);
 }
 

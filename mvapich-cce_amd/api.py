@@ -14,7 +14,7 @@ __all__ = [
     "MPI_Allreduce", "MPI_Reduce", "MPI_Reduce_scatter", "MPI_Scan", "MPI_Op_create", "MPI_Op_free", "op_create_device",
     "MPIR_call", "op_errno", "last_kernel", "last_kernel_symbol", "last_launch", "set_launch",
     "set_fortran_logical", "comm_reap", "host_register_enable", "host_unregister", "host_register_stats",
-    "host_hooks_active", "host_invalidate",
+    "host_hooks_active", "host_invalidate", "host_register_deferred",
     "MPI_Type_contiguous", "MPI_Type_commit", "MPI_Type_free", "MPI_Type_extent", "MPI_Type_size",
     "MPI_Type_vector", "MPI_Type_hvector", "MPI_Type_indexed", "MPI_Type_hindexed", "MPI_Type_struct",
     "MPI_Type_lb", "MPI_Type_ub", "type_layout", "type_set_handle", "type_pack", "type_unpack",
@@ -533,3 +533,13 @@ def host_register_stats():
     e, b, h, m = ctypes.c_long(), ctypes.c_size_t(), ctypes.c_long(), ctypes.c_long()
     coll().mvx_host_register_stats(ctypes.byref(e), ctypes.byref(b), ctypes.byref(h), ctypes.byref(m))
     return {"entries": e.value, "bytes": b.value, "hits": h.value, "misses": m.value}
+
+
+def host_register_deferred():
+    """{deferred, held, unregisters}: registrations a release dropped that
+    are not unregistered yet (a call still holds them, or no libmvx entry
+    has run since), registrations held by calls in flight, and the
+    hipHostUnregister calls made so far (mvx_host_register_deferred)."""
+    d, h, u = ctypes.c_long(), ctypes.c_long(), ctypes.c_long()
+    coll().mvx_host_register_deferred(ctypes.byref(d), ctypes.byref(h), ctypes.byref(u))
+    return {"deferred": d.value, "held": h.value, "unregisters": u.value}

@@ -136,6 +136,7 @@ static int run_on(mvx_comm_t *c, const call_t *k, hipStream_t st, int blocking)
     J.t = &t;
     c->keep = keep;
     rc = mvxi_run_job(c, &J, st, blocking);
+    mvxi_job_release(&J, rc);
     c->keep = 0;
     if (!plan_moves(Pp)) c->ran_exch = -1;   /* nothing crossed between ranks */
     return rc ? rc : vrc;
@@ -412,6 +413,7 @@ static int run_multi_on(mvx_comm_t *c, int coll, void *const *sendbufs,
     c->keep = verdict == MVX_ERR_OP_NOT_DEFINED;    /* the transfers of an undefined pair */
     if (plans[0].packed) rc = mvxi_run_job_packed(c, J, st, host);
     else rc = host ? mvxi_run_staged(c, J, st) : mvxi_run_device(c, J, st);
+    mvxi_job_release(J, rc);
     c->keep = 0;
     return rc;
 }

@@ -55,6 +55,10 @@ struct Type {
     // does not split into W-byte units
     int *dunits[3];
     long units[3];
+    // whole-word unpack (merge_ok): 0 not decided, 1 yes, -1 no; the map's
+    // reach [mlo, mhi) around the element origin
+    int merge;
+    long mlo, mhi;
 };
 
 static Type g_t[MVX_TYPE_DERIVED_MAX];
@@ -642,6 +646,129 @@ static int launch_units(const Type &t, int wi, const void *src, void *dst, long 
     return hipGetLastError() == hipSuccess ? MPI_SUCCESS : MPI_ERR_OTHER;
 }
 
+// ---- unpack by whole words ------------------------------------------------
+// The unit kernel's unpack stores W bytes per unit: where the type map
+// leaves holes inside a 64-byte DRAM sector, every such store is a partial
+// write the memory must merge with the sector's old bytes.  This variant
+// merges on the CU instead: a workgroup owns a 16-byte-aligned tile of the
+// destination, loads it whole into LDS, writes the tile's units (read from
+// the packed stream, contiguous per tile) over it in LDS, and stores the
+// tile back whole -- full-line reads and writes only.  The hole bytes go
+// back as they were read, so this is for destinations no one else writes
+// meanwhile (MVX_UNPACK_MERGE=0 keeps the byte-exact stores).  Words that
+// reach outside the hull of the whole buffer's type maps (its first and
+// last) are never written whole: their units are stored directly.
+#define MERGE_TILE 8192              // destination bytes per workgroup (LDS)
+#define MERGE_UNITS_LDS 2048
+
+template <int W>
+__global__ void __launch_bounds__(256)
+k_unpack_merge(const char *__restrict__ packed, char *__restrict__ dst, const int *__restrict__ uoff, long upe,
+               long n, long ext, long lo, long hi, uintptr_t a0, uintptr_t h0, uintptr_t h1, long D, long R)
+{
+    typedef typename UnitT<W>::t V;
+    __shared__ pu32x4 s_tile[MERGE_TILE / 16];
+    __shared__ int s_uoff[MERGE_UNITS_LDS];
+    const bool lds_units = upe <= MERGE_UNITS_LDS;
+    if (lds_units)
+        for (int u = threadIdx.x; u < (int)upe; u += 256) s_uoff[u] = uoff[u];
+    const uintptr_t t0 = a0 + (uintptr_t)blockIdx.x * MERGE_TILE;          // this tile's first word
+    const uintptr_t tend = t0 + MERGE_TILE < ((h1 + 15) & ~(uintptr_t)15) ? t0 + MERGE_TILE
+                                                                           : ((h1 + 15) & ~(uintptr_t)15);
+    const int nw = (int)((tend - t0) / 16);
+    for (int w = threadIdx.x; w < nw; w += 256)
+        s_tile[w] = __builtin_nontemporal_load((const pu32x4 *)(t0 + 16 * (uintptr_t)w));
+    __syncthreads();
+    // the elements whose maps reach into [t0, tend): relative to dst
+    const long a = (long)(t0 - (uintptr_t)dst), b = (long)(tend - (uintptr_t)dst);
+    long ilo = a - hi >= 0 ? (a - hi) / ext + 1 : 0;
+    long ihi = b - lo > 0 ? (b - lo + ext - 1) / ext : 0;
+    if (ihi > n) ihi = n;
+    const long qend = ihi * upe;
+    long q = ilo * upe + threadIdx.x;
+    long i = q / upe, j = q - i * upe;
+    for (; q < qend; q += 256) {
+        const long off = i * ext + (lds_units ? s_uoff[j] : uoff[j]);
+        if (off >= a && off < b) {
+            const V v = __builtin_nontemporal_load((const V *)(packed + q * W));
+            const uintptr_t at = (uintptr_t)dst + off, word = at & ~(uintptr_t)15;
+            if (word < h0 || word + 16 > h1) *(V *)at = v;                    // a word past the hull: its units only
+            else *(V *)((char *)s_tile + (at - t0)) = v;
+        }
+        i += D;
+        j += R;
+        if (j >= upe) { j -= upe; i++; }
+    }
+    __syncthreads();
+    for (int w = threadIdx.x; w < nw; w += 256) {
+        const uintptr_t at = t0 + 16 * (uintptr_t)w;
+        if (at >= h0 && at + 16 <= h1) __builtin_nontemporal_store(s_tile[w], (pu32x4 *)at);
+    }
+}
+
+// MVX_UNPACK_MERGE: 1 (default) unpack by whole words where the type's map
+// qualifies, 0 the unit kernel's byte-exact stores everywhere
+static int merge_on()
+{
+    static int on = -1;
+    if (on < 0) {
+        const char *e = getenv("MVX_UNPACK_MERGE");
+        on = e ? atoi(e) != 0 : 1;
+    }
+    return on;
+}
+
+// The map's reach around the element origin [lo, hi) and whether whole-word
+// unpack pays: the maps of neighbouring elements must not interleave (each
+// destination byte has one writer), and the map must leave holes inside 64-B
+// sectors (partial writes), with no 64-B sector of the hull wholly untouched
+// (one that a byte-exact unpack would not touch at all but the merge would
+// read and write).
+static bool merge_ok(const Type &t, long *lo, long *hi)
+{
+    if (t.map.empty() || t.extent <= 0) return false;
+    long l = t.map[0].off, h = t.map[0].off + t.map[0].len;
+    for (const Blk &b : t.map) {
+        if (b.off < l) l = b.off;
+        if (b.off + b.len > h) h = b.off + b.len;
+    }
+    *lo = l;
+    *hi = h;
+    if (h - l > t.extent) return false;
+    long g = t.extent, m = 64;
+    while (m) { const long r = g % m; g = m; m = r; }
+    const long reps = 64 / g, span = t.extent * reps;
+    if (span > (1L << 20)) return false;
+    std::vector<unsigned char> cov((size_t)span + 64, 0);
+    for (long r = 0; r < reps; ++r)
+        for (const Blk &b : t.map)
+            for (long o = 0; o < b.len; ++o) {
+                const long x = ((r * t.extent + b.off + o - l) % span + span) % span;
+                cov[(size_t)x] = 1;
+            }
+    bool partial = false;
+    for (long s = 0; s < span; s += 64) {
+        int c = 0;
+        for (long k = s; k < s + 64 && k < span; ++k) c += cov[(size_t)k];
+        if (c == 0) return false;
+        if (c < 64) partial = true;
+    }
+    return partial;
+}
+
+template <int W>
+static int launch_merge(Type &t, int wi, const void *src, void *dst, long count, long lo, long hi, hipStream_t st)
+{
+    const long upe = t.units[wi];
+    const uintptr_t h0 = (uintptr_t)dst + lo, h1 = (uintptr_t)dst + (count - 1) * t.extent + hi;
+    const uintptr_t a0 = h0 & ~(uintptr_t)15;
+    const long tiles = (long)((((h1 + 15) & ~(uintptr_t)15) - a0 + MERGE_TILE - 1) / MERGE_TILE);
+    if (tiles < 1 || tiles > INT32_MAX) return MPI_ERR_OTHER;
+    hipLaunchKernelGGL((k_unpack_merge<W>), dim3((unsigned)tiles), dim3(256), 0, st, (const char *)src, (char *)dst,
+                       (const int *)t.dunits[wi], upe, count, t.extent, lo, hi, a0, h0, h1, 256 / upe, 256 % upe);
+    return hipGetLastError() == hipSuccess ? MPI_SUCCESS : MPI_ERR_OTHER;
+}
+
 static int device_map(Type &t)
 {
     if (t.dmap) return MPI_SUCCESS;
@@ -686,6 +813,14 @@ static int pack(int h, const void *src, void *dst, size_t count, hipStream_t st,
         for (int wi = 0; units_on && wi < 3; ++wi) {
             const int W = Ws[wi];
             if (al % W || !unit_table(*t, W, wi)) continue;
+            if (!packing && merge_on()) {
+                if (!t->merge) t->merge = merge_ok(*t, &t->mlo, &t->mhi) ? 1 : -1;
+                if (t->merge > 0) {
+                    if (W == 16) return launch_merge<16>(*t, wi, src, dst, (long)count, t->mlo, t->mhi, st);
+                    if (W == 8) return launch_merge<8>(*t, wi, src, dst, (long)count, t->mlo, t->mhi, st);
+                    return launch_merge<4>(*t, wi, src, dst, (long)count, t->mlo, t->mhi, st);
+                }
+            }
             if (W == 16) return packing ? launch_units<true, 16>(*t, wi, src, dst, (long)count, st)
                                         : launch_units<false, 16>(*t, wi, src, dst, (long)count, st);
             if (W == 8) return packing ? launch_units<true, 8>(*t, wi, src, dst, (long)count, st)

@@ -210,22 +210,40 @@ int mvxi_recv_ranges(const mvx_plan *Q, mvx_range *v)
 
 
 /* the buffers' kinds, one pointer query each (pageable ranges may come back
- * pinned from the registration cache); returns 1 if any is host memory */
+ * pinned from the registration cache, held for the job until
+ * mvxi_job_release); returns 1 if any is host memory */
 int mvxi_job_kinds(job_t *J)
 {
     int r, host = 0;
     if (!J->kinds) {
         for (r = 0; r < J->nr; r++) {
             const size_t E = (size_t)J->P[r].esize;
-            J->skind[r] = J->nsend[r] > 0 ? mvxi_buf_kind_range(J->send[r], (size_t)J->nsend[r] * E)
-                                          : MVX_BUF_DEVICE;
-            J->rkind[r] = J->nrecv[r] > 0 ? mvxi_buf_kind_range(J->recv[r], (size_t)J->nrecv[r] * E)
-                                          : MVX_BUF_DEVICE;
+            J->shold[r] = J->rhold[r] = 0;
+            J->skind[r] = J->nsend[r] > 0
+                              ? mvxi_buf_kind_hold(J->send[r], (size_t)J->nsend[r] * E, &J->shold[r])
+                              : MVX_BUF_DEVICE;
+            J->rkind[r] = J->nrecv[r] > 0
+                              ? mvxi_buf_kind_hold(J->recv[r], (size_t)J->nrecv[r] * E, &J->rhold[r])
+                              : MVX_BUF_DEVICE;
         }
         J->kinds = 1;
     }
     for (r = 0; r < J->nr; r++) host |= J->skind[r] != MVX_BUF_DEVICE || J->rkind[r] != MVX_BUF_DEVICE;
     return host;
+}
+
+void mvxi_job_release(job_t *J, int rc)
+{
+    int r, any = 0;
+    if (!J->kinds) return;
+    for (r = 0; r < J->nr; r++) any |= J->shold[r] || J->rhold[r];
+    if (!any) return;
+    if (rc != MPI_SUCCESS && hipDeviceSynchronize() != hipSuccess) (void)hipGetLastError();
+    for (r = 0; r < J->nr; r++) {
+        mvxi_buf_release(J->shold[r]);
+        mvxi_buf_release(J->rhold[r]);
+        J->shold[r] = J->rhold[r] = 0;
+    }
 }
 
 
@@ -528,9 +546,10 @@ static int graph_match(const graph_ent_t *g, const mvx_comm_t *c, const job_t *J
  * loop, dies within 30 rounds on HIP 7.0 and never on 7.2; kept alive, or
  * without the fork, it never dies; no RCCL needed).  So graphs are destroyed
  * mid-life again -- before the pool they were captured on is freed, and the
- * least recently used one when every slot holds a graph -- where the runtime
- * allows (mvxi_graph_evict_default): any graph from HIP 7.2 on, only
- * single-branch ones before it (PIPE's forked captures are retired there).
+ * least recently used one when every slot holds a graph and a job seen
+ * twice is about to be captured -- where the runtime allows
+ * (mvxi_graph_evict_default): any graph from HIP 7.2 on, only single-branch
+ * ones before it (PIPE's forked captures are retired there).
  * MVX_GRAPH_CACHE=n (<= 32) caps the graphs a communicator holds. */
 
 static void graph_destroy(graph_ent_t *g)
@@ -539,6 +558,7 @@ static void graph_destroy(graph_ent_t *g)
         gtrace("destroy graph of variant", g->exch);
         hipGraphExecDestroy(g->exec);
     }
+    if (g->done) hipEventDestroy(g->done);
     memset(g, 0, sizeof *g);
 }
 
@@ -568,7 +588,10 @@ void mvxi_graphs_clear(mvx_comm_t *c)
 {
     int i;
     if (!c->w) return;
-    for (i = 0; i < GRAPH_CACHE; i++) graph_destroy(&c->w->graphs[i]);
+    for (i = 0; i < GRAPH_CACHE; i++) {
+        graph_destroy(&c->w->graphs[i]);
+        memset(&c->w->seen[i], 0, sizeof c->w->seen[i]);
+    }
 }
 
 /* may this graph's exec be destroyed now (mvxi_graph_evict_default)? */
@@ -618,9 +641,9 @@ int mvxi_grow_pool(mvx_comm_t *c, size_t need)
         int gone = 0;
         for (i = 0; i < GRAPH_CACHE; i++) {
             graph_ent_t *g = &c->w->graphs[i];
+            if (c->w->seen[i].pool == c->pool) memset(&c->w->seen[i], 0, sizeof c->w->seen[i]);
             if (g->pool != c->pool) continue;
-            if (g->state == G_SEEN) memset(g, 0, sizeof *g);
-            else if (g->state == G_LIVE) { g->state = G_RETIRED; gone += graph_evictable(c, g); }
+            if (g->state == G_LIVE) { g->state = G_RETIRED; gone += graph_evictable(c, g); }
         }
         if (gone) {
             hipDeviceSynchronize();
@@ -661,21 +684,25 @@ static int graph_streams(mvx_comm_t *c)
     return MPI_SUCCESS;
 }
 
-static int graph_launch(mvx_comm_t *c, hipGraphExec_t x, hipStream_t st)
+/* launch g's exec on `st` (the null stream: forked onto the graph stream and
+ * joined back) and record g->done where it ran */
+static int graph_launch(mvx_comm_t *c, graph_ent_t *g, hipStream_t st)
 {
+    hipStream_t on = st ? st : c->gstream;
     if (st) {
         gtrace("launch on the caller's stream", 0);
-        return hipGraphLaunch(x, st) == hipSuccess ? MPI_SUCCESS : MPI_ERR_OTHER;
+        if (hipGraphLaunch(g->exec, st) != hipSuccess) return MPI_ERR_OTHER;
+    } else {
+        gtrace("launch: fork from the null stream", 0);
+        if (hipEventRecord(c->gev[0], st) != hipSuccess || hipStreamWaitEvent(c->gstream, c->gev[0], 0) != hipSuccess)
+            return MPI_ERR_OTHER;
+        gtrace("launch: hipGraphLaunch on the graph stream", 0);
+        if (hipGraphLaunch(g->exec, c->gstream) != hipSuccess) return MPI_ERR_OTHER;
+        gtrace("launch: join to the null stream", 0);
+        if (hipEventRecord(c->gev[1], c->gstream) != hipSuccess || hipStreamWaitEvent(st, c->gev[1], 0) != hipSuccess)
+            return MPI_ERR_OTHER;
     }
-    gtrace("launch: fork from the null stream", 0);
-    if (hipEventRecord(c->gev[0], st) != hipSuccess || hipStreamWaitEvent(c->gstream, c->gev[0], 0) != hipSuccess)
-        return MPI_ERR_OTHER;
-    gtrace("launch: hipGraphLaunch on the graph stream", 0);
-    if (hipGraphLaunch(x, c->gstream) != hipSuccess) return MPI_ERR_OTHER;
-    gtrace("launch: join to the null stream", 0);
-    if (hipEventRecord(c->gev[1], c->gstream) != hipSuccess || hipStreamWaitEvent(st, c->gev[1], 0) != hipSuccess)
-        return MPI_ERR_OTHER;
-    return MPI_SUCCESS;
+    return hipEventRecord(g->done, on) == hipSuccess ? MPI_SUCCESS : MPI_ERR_OTHER;
 }
 
 /* MVX_GRAPH_TRACE=1: each capture step on stderr (diagnostics) */
@@ -725,61 +752,86 @@ static int graph_capture(mvx_comm_t *c, const job_t *J, hipStream_t cs, hipGraph
     return MPI_SUCCESS;
 }
 
+/* Graph slots hold captured graphs only; jobs seen once wait in a table of
+ * their own (mvx_work.seen, least recently seen replaced).  A job runs
+ * eagerly at its first sighting and is captured at its second: only then,
+ * when every slot holds a graph, is the least recently used evictable one
+ * destroyed -- after its own last launch completed (its done event), not
+ * the whole device.  A communicator with more distinct jobs than slots thus
+ * keeps its graphs instead of trading one for every new job it sees. */
 static int run_device_graph(mvx_comm_t *c, const job_t *J, hipStream_t st)
 {
     mvx_work *w = mvxi_work(c);
     const unsigned long long h = graph_hash(c, J, st);
-    graph_ent_t *g = NULL, *slot = NULL;
+    graph_ent_t *g = NULL, *slot = NULL, *seen = NULL, *sslot = NULL, *lru = NULL;
     hipGraphExec_t x;
     int i, rc, forked = 1;
-    graph_ent_t *lru = NULL;
     if (!w || (!st && graph_streams(c))) return run_device_eager(c, J, st);
     for (i = 0; i < c->graph_cap; i++) {
         graph_ent_t *e = &w->graphs[i];
         if (graph_match(e, c, J, st, h)) { g = e; break; }
-        /* a slot for a new job: a free one, else the least recently seen-once */
-        if (e->state == G_FREE && (!slot || slot->state != G_FREE)) slot = e;
-        else if (e->state == G_SEEN && (!slot || (slot->state == G_SEEN && e->stamp < slot->stamp))) slot = e;
+        if (e->state == G_FREE && !slot) slot = e;
         if (e->state == G_LIVE && graph_evictable(c, e) && (!lru || e->stamp < lru->stamp)) lru = e;
     }
-    if (!g && !slot && lru) {                                  /* every slot holds a graph: evict the LRU */
-        hipDeviceSynchronize();
-        graph_evict(c, lru);
-        slot = lru;
-    }
-    if (g && g->state == G_LIVE) {                             /* replay */
+    if (g) {                                                   /* replay */
         g->stamp = ++w->graph_clock;
         c->ran_exch = g->ran_exch;
         c->last_graph = 1;
-        return graph_launch(c, g->exec, st);
+        return graph_launch(c, g, st);
     }
-    if (!g) {                                                  /* first sighting: eager */
+    for (i = 0; i < GRAPH_CACHE; i++) {
+        graph_ent_t *e = &w->seen[i];
+        if (graph_match(e, c, J, st, h)) { seen = e; break; }
+        if (!sslot || (sslot->state != G_FREE && (e->state == G_FREE || e->stamp < sslot->stamp))) sslot = e;
+    }
+    if (!seen) {                                               /* first sighting: eager */
         c->last_graph = 0;
         rc = run_device_eager(c, J, st);
-        if (rc || !slot) return rc;                            /* no slot: every one holds a graph */
-        memset(slot, 0, sizeof *slot);
-        slot->state = G_SEEN;
-        slot->hash = graph_hash(c, J, st);                     /* the pool as the call left it */
-        slot->plan = J->P[0];
-        slot->send = J->send[0]; slot->recv = J->recv[0]; slot->st = st; slot->pool = c->pool;
-        slot->exch = c->exch; slot->slices = c->exch_slices; slot->keep = c->keep;
-        slot->stamp = ++w->graph_clock;
+        if (rc) return rc;
+        memset(sslot, 0, sizeof *sslot);
+        sslot->state = G_SEEN;
+        sslot->hash = graph_hash(c, J, st);                    /* the pool as the call left it */
+        sslot->plan = J->P[0];
+        sslot->send = J->send[0]; sslot->recv = J->recv[0]; sslot->st = st; sslot->pool = c->pool;
+        sslot->exch = c->exch; sslot->slices = c->exch_slices; sslot->keep = c->keep;
+        sslot->stamp = ++w->graph_clock;
         return MPI_SUCCESS;
     }
-    rc = graph_capture(c, J, st ? st : c->gstream, &x, &forked);   /* second sighting: capture */
-    if (rc) {
-        c->graph_error = rc;
-        memset(g, 0, sizeof *g);
+    /* second sighting: capture, into a free slot or the LRU graph's */
+    if (!slot && lru) {
+        if (lru->done && hipEventSynchronize(lru->done) != hipSuccess) (void)hipGetLastError();
+        graph_evict(c, lru);
+        slot = lru;
+    }
+    memset(seen, 0, sizeof *seen);
+    if (!slot) {                                               /* every slot holds a graph it may not destroy */
         c->last_graph = 0;
         return run_device_eager(c, J, st);
     }
-    g->exec = x;
-    g->forked = forked;
-    g->state = G_LIVE;
-    g->ran_exch = c->ran_exch;
-    g->stamp = ++w->graph_clock;
+    if (hipEventCreateWithFlags(&slot->done, hipEventDisableTiming) != hipSuccess) {
+        (void)hipGetLastError();
+        slot->done = NULL;
+        c->last_graph = 0;
+        return run_device_eager(c, J, st);
+    }
+    rc = graph_capture(c, J, st ? st : c->gstream, &x, &forked);
+    if (rc) {
+        c->graph_error = rc;
+        graph_destroy(slot);
+        c->last_graph = 0;
+        return run_device_eager(c, J, st);
+    }
+    slot->state = G_LIVE;
+    slot->hash = graph_hash(c, J, st);
+    slot->plan = J->P[0];
+    slot->send = J->send[0]; slot->recv = J->recv[0]; slot->st = st; slot->pool = c->pool;
+    slot->exch = c->exch; slot->slices = c->exch_slices; slot->keep = c->keep;
+    slot->exec = x;
+    slot->forked = forked;
+    slot->ran_exch = c->ran_exch;
+    slot->stamp = ++w->graph_clock;
     c->last_graph = 2;
-    rc = graph_launch(c, x, st);
+    rc = graph_launch(c, slot, st);
     gtrace("first launch, rc", rc);
     return rc;
 }

@@ -25,8 +25,10 @@
  * (round 4), and no CPU-side check can see the free
  * afterwards.  So, as the reference learns of released memory through its
  * hooks (mem_hooks.c), libmvx.so interposes the calls that release memory
- * (free, realloc, munmap, mremap, madvise, sbrk; below) and drops every
- * registration inside a released range first.  Mode 1 of the cache needs
+ * (free, realloc, munmap, mremap, madvise, sbrk; below) and unlinks every
+ * registration a release hits before the release; the unregistration itself
+ * is deferred to the next libmvx entry and waits for the calls still using
+ * the registration (dreg.c's deferred, refcounted scheme).  Mode 1 of the cache needs
  * those hooks in effect; mode 2 is for callers that report releases
  * themselves (mvx_host_unregister / mvx_host_invalidate: a dlopen'ed
  * library, or a host MPI whose own hooks call mvx_host_invalidate).
@@ -43,9 +45,15 @@
 
 #include "mvx_internal.h"
 
+static void reg_flush(void);
+
+/* (the registration cache's deferred releases are unregistered first: a
+ * stale registration would make HIP report pages it no longer maps as
+ * page-locked) */
 int mvx_buf_kind(const void *p)
 {
     hipPointerAttribute_t a;
+    reg_flush();
     if (!p) return MVX_BUF_PAGEABLE;
     if (hipPointerGetAttributes(&a, p) != hipSuccess) {
         (void)hipGetLastError();
@@ -198,28 +206,63 @@ int mvx_copy_threads(void)
 }
 
 /* ---- the registration cache ------------------------------------------------
- * Entries are page-aligned [base, end) ranges.  No HIP call is made while
- * the table's mutex is held: entries leave the table under the lock and are
- * unregistered after it is released (the release hooks below run inside
- * free(), which HIP's own threads call too, so they must never wait for a
- * thread that is inside HIP). */
+ * Entries are page-aligned [base, end) ranges -- the pages hipHostRegister
+ * locked -- with the span [ulo, uhi) of the buffers the calls asked for.
+ * The rules follow MVAPICH's dreg (mpid/ch_gen2/dreg.c):
+ *   - no HIP call is made while the table's mutex is held;
+ *   - a release never calls into HIP where it is reported (the hooks run
+ *     inside free(), on any thread, HIP's own included): it only unlinks the
+ *     entries the released memory overlaps, so that no later call finds
+ *     them, and moves them to a deferred list (find_and_free_dregs_inside,
+ *     dreg.c:1063-1080).  Deferred entries are unregistered at the next
+ *     libmvx entry (reg_flush: every buffer-kind query, every registration,
+ *     the end of every call that held one; flush_dereg_mrs_external,
+ *     dreg.c:678-767);
+ *   - an entry a call is using is never unregistered: a call takes a hold
+ *     when it finds or makes the registration (mvxi_buf_kind_hold) and drops
+ *     it after its last DMA (mvxi_buf_release); a deferred entry that is
+ *     still held waits for its last hold (dreg.c:725-733, "still being
+ *     referenced by other pending MPI operations"), and eviction and merging
+ *     pass held entries by;
+ *   - a release reported on a thread that is inside our own registration
+ *     calls (HIP freeing its own memory inside hipHostRegister /
+ *     hipHostUnregister) records nothing, as have_dereg() / have_dreg() make
+ *     the reference's hook return (dreg.c:1066).
+ * Which releases drop an entry: one that releases pages (munmap, mremap,
+ * madvise, negative sbrk, mvx_host_invalidate) drops every entry whose
+ * pages it overlaps; free / realloc of a heap block drops the entries whose
+ * buffer span the block overlaps.  A block beside a registered buffer that
+ * only shares its boundary page keeps the registration: no allocator gives
+ * back a page that still holds a live buffer, so those pages stay mapped
+ * (and pinned) for as long as the buffer lives. */
 
 #define REG_MAX 64
+#define REG_DEFER (2 * REG_MAX)    /* new entries are refused while REG_MAX are deferred */
+#define REG_FLY 8                  /* registrations in progress (hipHostRegister outside the lock) */
 #define PAGE 4096UL
-typedef struct { uintptr_t base, end; unsigned long stamp; } reg_t;
+typedef struct { uintptr_t base, end, ulo, uhi; unsigned long stamp, id; int hold; } reg_t;
+typedef struct { uintptr_t base, end, ulo, uhi; int used, stale; } reg_fly_t;
 static struct {
     pthread_mutex_t mu;
     int init, on, dry;
     size_t min_bytes, max_bytes, total;
-    unsigned long clock, hits, misses, evictions, failures, invalidations;
-    int n;
-    reg_t e[REG_MAX];
-} g_reg = { PTHREAD_MUTEX_INITIALIZER, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, {{0, 0, 0}} };
+    unsigned long clock, next_id, hits, misses, evictions, failures, invalidations;
+    int n, nd;
+    reg_t e[REG_MAX];              /* the table: registered, findable */
+    reg_t d[REG_DEFER];            /* deferred: released, still registered until unheld and flushed */
+    reg_fly_t fly[REG_FLY];
+} g_reg = { PTHREAD_MUTEX_INITIALIZER };
 
-/* read without the lock by the release hooks: entries exist, and the span
- * [lo, hi) covering all of them (a superset while entries change) */
-static volatile int g_reg_live;
+/* read without the lock: entries or registrations in progress exist, and the
+ * span [lo, hi) covering all of them (a superset while they change); the
+ * deferred count (reg_flush's fast path); HIP unregister calls made (or, dry,
+ * that would have been) */
+static volatile int g_reg_live, g_reg_nd;
 static volatile uintptr_t g_reg_lo, g_reg_hi;
+static volatile long g_reg_unregisters;
+
+/* > 0 while this thread is inside our own hipHostRegister / Unregister */
+static __thread int t_in_reg;
 
 static void reg_env(void)
 {
@@ -241,94 +284,146 @@ static void reg_env(void)
 static void reg_span_locked(void)
 {
     uintptr_t lo = UINTPTR_MAX, hi = 0;
-    int i;
+    int i, live = g_reg.n;
     for (i = 0; i < g_reg.n; i++) {
         if (g_reg.e[i].base < lo) lo = g_reg.e[i].base;
         if (g_reg.e[i].end > hi) hi = g_reg.e[i].end;
     }
-    __atomic_store_n(&g_reg_lo, g_reg.n ? lo : UINTPTR_MAX, __ATOMIC_RELAXED);
-    __atomic_store_n(&g_reg_hi, g_reg.n ? hi : 0, __ATOMIC_RELAXED);
-    __atomic_store_n(&g_reg_live, g_reg.n, __ATOMIC_RELEASE);
+    for (i = 0; i < REG_FLY; i++)
+        if (g_reg.fly[i].used) {
+            live++;
+            if (g_reg.fly[i].base < lo) lo = g_reg.fly[i].base;
+            if (g_reg.fly[i].end > hi) hi = g_reg.fly[i].end;
+        }
+    __atomic_store_n(&g_reg_lo, live ? lo : UINTPTR_MAX, __ATOMIC_RELAXED);
+    __atomic_store_n(&g_reg_hi, live ? hi : 0, __ATOMIC_RELAXED);
+    __atomic_store_n(&g_reg_nd, g_reg.nd, __ATOMIC_RELEASE);
+    __atomic_store_n(&g_reg_live, live, __ATOMIC_RELEASE);
 }
 
-/* entries leaving the table, unregistered once the lock is dropped */
-typedef struct { int n; reg_t e[REG_MAX]; } reg_out_t;
+/* entries leaving the table now, unregistered once the lock is dropped */
+typedef struct { int n; uintptr_t base[REG_DEFER + REG_MAX]; } reg_out_t;
 
 static void reg_take_locked(int i, reg_out_t *out)
 {
-    out->e[out->n++] = g_reg.e[i];
+    out->base[out->n++] = g_reg.e[i].base;
     g_reg.total -= g_reg.e[i].end - g_reg.e[i].base;
     g_reg.e[i] = g_reg.e[--g_reg.n];
+}
+
+/* entry i leaves the table for the deferred list (no HIP call) */
+static void reg_defer_locked(int i)
+{
+    g_reg.d[g_reg.nd++] = g_reg.e[i];
+    g_reg.total -= g_reg.e[i].end - g_reg.e[i].base;
+    g_reg.e[i] = g_reg.e[--g_reg.n];
+}
+
+static void reg_unregister(uintptr_t base, int dry)
+{
+    __atomic_add_fetch(&g_reg_unregisters, 1, __ATOMIC_RELAXED);
+    if (dry) return;
+    t_in_reg++;
+    (void)hipHostUnregister((void *)base);
+    (void)hipGetLastError();
+    t_in_reg--;
 }
 
 static void reg_release(const reg_out_t *out, int dry)
 {
     int i;
-    if (dry) return;
-    for (i = 0; i < out->n; i++) {
-        (void)hipHostUnregister((void *)out->e[i].base);
-        (void)hipGetLastError();
-    }
+    for (i = 0; i < out->n; i++) reg_unregister(out->base[i], dry);
 }
 
-/* every entry overlapping [lo, hi) leaves the table and is unregistered */
-static int reg_invalidate(uintptr_t lo, uintptr_t hi)
+/* unregister every deferred entry no call holds any more */
+static void reg_flush(void)
 {
     reg_out_t out;
     int i, dry;
+    if (!__atomic_load_n(&g_reg_nd, __ATOMIC_ACQUIRE)) return;
     out.n = 0;
     pthread_mutex_lock(&g_reg.mu);
-    for (i = g_reg.n - 1; i >= 0; i--)
-        if (g_reg.e[i].base < hi && lo < g_reg.e[i].end) reg_take_locked(i, &out);
-    g_reg.invalidations += (unsigned long)out.n;
+    for (i = g_reg.nd - 1; i >= 0; i--)
+        if (g_reg.d[i].hold == 0) {
+            out.base[out.n++] = g_reg.d[i].base;
+            g_reg.d[i] = g_reg.d[--g_reg.nd];
+        }
     reg_span_locked();
     dry = g_reg.dry;
     pthread_mutex_unlock(&g_reg.mu);
     reg_release(&out, dry);
-    return out.n;
 }
 
+static int overlaps(uintptr_t a0, uintptr_t a1, uintptr_t b0, uintptr_t b1) { return a0 < b1 && b0 < a1; }
+
+/* A release of [lo, hi): unlink what it hits (reg_t rules above), mark the
+ * registrations in progress it hits stale.  `block`: a heap block (free /
+ * realloc), tested against the buffer spans; else pages.  No HIP call. */
+static int reg_unlink(uintptr_t lo, uintptr_t hi, int block)
+{
+    int i, n = 0;
+    if (!block) {
+        lo &= ~(PAGE - 1);
+        hi = (hi + PAGE - 1) & ~(PAGE - 1);
+    }
+    pthread_mutex_lock(&g_reg.mu);
+    for (i = g_reg.n - 1; i >= 0; i--) {
+        const reg_t *e = &g_reg.e[i];
+        if (block ? overlaps(e->ulo, e->uhi, lo, hi) : overlaps(e->base, e->end, lo, hi)) {
+            reg_defer_locked(i);
+            n++;
+        }
+    }
+    for (i = 0; i < REG_FLY; i++) {
+        reg_fly_t *f = &g_reg.fly[i];
+        if (f->used && (block ? overlaps(f->ulo, f->uhi, lo, hi) : overlaps(f->base, f->end, lo, hi))) f->stale = 1;
+    }
+    g_reg.invalidations += (unsigned long)n;
+    reg_span_locked();
+    pthread_mutex_unlock(&g_reg.mu);
+    return n;
+}
+
+/* the host MPI's hooks report a release (mem_hooks.c -> dreg.c:1063): they
+ * run inside the release, so the entries are only unlinked here and
+ * unregistered at the next libmvx entry */
 int mvx_host_invalidate(const void *addr, size_t bytes)
 {
     const uintptr_t a = (uintptr_t)addr;
     if (!bytes || !__atomic_load_n(&g_reg_live, __ATOMIC_ACQUIRE)) return 0;
-    return reg_invalidate(a & ~(PAGE - 1), a + bytes);
+    return reg_unlink(a, a + bytes, 0);
 }
 
 int mvx_host_register_enable(int on, size_t max_bytes)
 {
-    reg_out_t out;
-    int dry;
     if (on < 0 || on > 2) return MPI_ERR_ARG;
     if (on == 1 && !mvx_host_hooks_active()) return MPI_ERR_OTHER;
-    out.n = 0;
     pthread_mutex_lock(&g_reg.mu);
     reg_env();
     g_reg.on = on;
     if (max_bytes) g_reg.max_bytes = max_bytes;
     if (!g_reg.on)
-        while (g_reg.n) reg_take_locked(g_reg.n - 1, &out);
+        while (g_reg.n) reg_defer_locked(g_reg.n - 1);
     reg_span_locked();
-    dry = g_reg.dry;
     pthread_mutex_unlock(&g_reg.mu);
-    reg_release(&out, dry);
+    reg_flush();
     return 0;
 }
 
 int mvx_host_unregister(const void *addr)
 {
     const uintptr_t a = (uintptr_t)addr;
-    reg_out_t out;
-    int i, dry;
-    out.n = 0;
+    int i, n = 0;
     pthread_mutex_lock(&g_reg.mu);
     for (i = g_reg.n - 1; i >= 0; i--)
-        if (g_reg.e[i].base <= a && a < g_reg.e[i].end) reg_take_locked(i, &out);
+        if (g_reg.e[i].base <= a && a < g_reg.e[i].end) {
+            reg_defer_locked(i);          /* unregistered once no call holds it */
+            n++;
+        }
     reg_span_locked();
-    dry = g_reg.dry;
     pthread_mutex_unlock(&g_reg.mu);
-    reg_release(&out, dry);
-    return out.n ? 0 : MPI_ERR_ARG;
+    reg_flush();
+    return n ? 0 : MPI_ERR_ARG;
 }
 
 int mvx_host_register_stats(long *entries, size_t *bytes, long *hits, long *misses)
@@ -352,84 +447,169 @@ long mvx_host_register_invalidations(void)
     return n;
 }
 
-/* Register [p, p + bytes) (page-widened) in the cache; MVX_BUF_PINNED when
- * the range is (now) registered, else what mvx_buf_kind says.  `k` is p's
- * kind as mvx_buf_kind reported it. */
-static int reg_range(const void *p, size_t bytes, int k)
+int mvx_host_register_deferred(long *deferred, long *held, long *unregisters)
 {
+    int i;
+    long h = 0;
+    pthread_mutex_lock(&g_reg.mu);
+    for (i = 0; i < g_reg.n; i++) h += g_reg.e[i].hold > 0;
+    for (i = 0; i < g_reg.nd; i++) h += g_reg.d[i].hold > 0;
+    if (deferred) *deferred = g_reg.nd;
+    if (held) *held = h;
+    pthread_mutex_unlock(&g_reg.mu);
+    if (unregisters) *unregisters = __atomic_load_n(&g_reg_unregisters, __ATOMIC_RELAXED);
+    return 0;
+}
+
+/* Register [p, p + bytes) (page-widened) in the cache; MVX_BUF_PINNED when
+ * the range is (now) registered, else what mvx_buf_kind says, or
+ * MVX_BUF_PAGEABLE where the pages are under a registration the cache cannot
+ * hand out (deferred, held by a merge candidate, in progress elsewhere) --
+ * the bounce path then copies with the CPU.  `k` is p's kind as mvx_buf_kind
+ * reported it (after a flush).  With `id`, a call's hold is taken on the
+ * entry and its id stored (0: none). */
+static int reg_range(const void *p, size_t bytes, int k, unsigned long *id)
+{
+    const uintptr_t ulo = (uintptr_t)p, uhi = (uintptr_t)p + bytes;
     uintptr_t base, end;
     reg_out_t out;
-    int i, cover = -1, overlap = 0, dry, ok;
+    int i, cover = -1, overlap = 0, dry, ok, f = -1, conflict;
+    hipError_t hr = hipSuccess;
+    if (id) *id = 0;
     pthread_mutex_lock(&g_reg.mu);
     reg_env();
     if (!g_reg.on && !g_reg.n) { pthread_mutex_unlock(&g_reg.mu); return k; }
-    base = (uintptr_t)p & ~(PAGE - 1);
-    end = ((uintptr_t)p + bytes + PAGE - 1) & ~(PAGE - 1);
+    base = ulo & ~(PAGE - 1);
+    end = (uhi + PAGE - 1) & ~(PAGE - 1);
     for (i = 0; i < g_reg.n; i++) {
         if (g_reg.e[i].base <= base && end <= g_reg.e[i].end) cover = i;
-        else if (g_reg.e[i].base < end && base < g_reg.e[i].end) overlap = 1;
+        else if (overlaps(g_reg.e[i].base, g_reg.e[i].end, base, end)) overlap = 1;
     }
     if (cover >= 0) {                                   /* dreg_find */
-        g_reg.e[cover].stamp = ++g_reg.clock;
+        reg_t *e = &g_reg.e[cover];
+        e->stamp = ++g_reg.clock;
+        if (ulo < e->ulo) e->ulo = ulo;
+        if (uhi > e->uhi) e->uhi = uhi;
         g_reg.hits++;
+        if (id) { e->hold++; *id = e->id; }
         pthread_mutex_unlock(&g_reg.mu);
         return MVX_BUF_PINNED;
     }
+    for (i = 0; i < g_reg.nd; i++)                       /* released pages still pinned for a call */
+        if (overlaps(g_reg.d[i].base, g_reg.d[i].end, base, end)) { pthread_mutex_unlock(&g_reg.mu); return MVX_BUF_PAGEABLE; }
+    for (i = 0; i < REG_FLY; i++)
+        if (g_reg.fly[i].used && overlaps(g_reg.fly[i].base, g_reg.fly[i].end, base, end)) {
+            pthread_mutex_unlock(&g_reg.mu);
+            return MVX_BUF_PAGEABLE;
+        }
     if (k == MVX_BUF_PINNED && !overlap) {              /* the caller's own page-locked memory */
         pthread_mutex_unlock(&g_reg.mu);
         return k;
     }
     /* a range that runs past a registration of ours: the union replaces it
-     * (a DMA must never read past the pinned pages) */
-    out.n = 0;
-    for (i = g_reg.n - 1; i >= 0; i--)
-        if (g_reg.e[i].base < end && base < g_reg.e[i].end) {
-            if (g_reg.e[i].base < base) base = g_reg.e[i].base;
-            if (g_reg.e[i].end > end) end = g_reg.e[i].end;
-            reg_take_locked(i, &out);
+     * (a DMA must never read past the pinned pages) -- unless a call is
+     * using that registration */
+    for (i = 0; i < g_reg.n; i++)
+        if (g_reg.e[i].hold && overlaps(g_reg.e[i].base, g_reg.e[i].end, base, end)) {
+            pthread_mutex_unlock(&g_reg.mu);
+            return MVX_BUF_PAGEABLE;
         }
-    ok = g_reg.on && end - base >= g_reg.min_bytes && end - base <= g_reg.max_bytes;
-    while (ok && g_reg.n && (g_reg.n == REG_MAX || g_reg.total + (end - base) > g_reg.max_bytes)) {
-        int lru = 0;                                    /* evict the least recently used */
-        for (i = 1; i < g_reg.n; i++)
-            if (g_reg.e[i].stamp < g_reg.e[lru].stamp) lru = i;
-        reg_take_locked(lru, &out);
-        g_reg.evictions++;
+    out.n = 0;
+    {
+        uintptr_t u0 = ulo, u1 = uhi;
+        for (i = g_reg.n - 1; i >= 0; i--)
+            if (overlaps(g_reg.e[i].base, g_reg.e[i].end, base, end)) {
+                if (g_reg.e[i].base < base) base = g_reg.e[i].base;
+                if (g_reg.e[i].end > end) end = g_reg.e[i].end;
+                if (g_reg.e[i].ulo < u0) u0 = g_reg.e[i].ulo;
+                if (g_reg.e[i].uhi > u1) u1 = g_reg.e[i].uhi;
+                reg_take_locked(i, &out);
+            }
+        ok = g_reg.on && end - base >= g_reg.min_bytes && end - base <= g_reg.max_bytes && g_reg.nd < REG_MAX;
+        while (ok && g_reg.n && (g_reg.n == REG_MAX || g_reg.total + (end - base) > g_reg.max_bytes)) {
+            int lru = -1;                               /* evict the least recently used unheld entry */
+            for (i = 0; i < g_reg.n; i++)
+                if (!g_reg.e[i].hold && (lru < 0 || g_reg.e[i].stamp < g_reg.e[lru].stamp)) lru = i;
+            if (lru < 0) { ok = 0; break; }
+            reg_take_locked(lru, &out);
+            g_reg.evictions++;
+        }
+        for (i = 0; ok && i < REG_FLY; i++)
+            if (!g_reg.fly[i].used) { f = i; break; }
+        if (f < 0) ok = 0;
+        if (ok) {
+            g_reg.misses++;
+            g_reg.fly[f].base = base; g_reg.fly[f].end = end;
+            g_reg.fly[f].ulo = u0; g_reg.fly[f].uhi = u1;
+            g_reg.fly[f].used = 1; g_reg.fly[f].stale = 0;
+        }
     }
-    if (ok) g_reg.misses++;
     reg_span_locked();
     dry = g_reg.dry;
     pthread_mutex_unlock(&g_reg.mu);
     reg_release(&out, dry);
     if (!ok) return mvx_buf_kind(p);
-    if (!dry && hipHostRegister((void *)base, end - base, hipHostRegisterDefault) != hipSuccess) {   /* dreg_register */
-        (void)hipGetLastError();
-        pthread_mutex_lock(&g_reg.mu);
-        g_reg.failures++;
-        pthread_mutex_unlock(&g_reg.mu);
-        return mvx_buf_kind(p);
+    if (!dry) {                                          /* dreg_register */
+        t_in_reg++;
+        hr = hipHostRegister((void *)base, end - base, hipHostRegisterDefault);
+        t_in_reg--;
+        if (hr != hipSuccess) (void)hipGetLastError();
     }
     pthread_mutex_lock(&g_reg.mu);
-    if (g_reg.n == REG_MAX) {                           /* filled meanwhile: keep it out */
-        pthread_mutex_unlock(&g_reg.mu);
-        if (!dry) (void)hipHostUnregister((void *)base);
-        return mvx_buf_kind(p);
+    {
+        reg_fly_t *fl = &g_reg.fly[f];
+        /* meanwhile: a release of these pages (stale), another entry over
+         * them, or the table / the byte budget filled */
+        conflict = fl->stale || g_reg.n == REG_MAX || g_reg.total + (end - base) > g_reg.max_bytes;
+        for (i = 0; !conflict && i < g_reg.n; i++) conflict = overlaps(g_reg.e[i].base, g_reg.e[i].end, base, end);
+        fl->used = 0;
+        if (hr != hipSuccess) {
+            g_reg.failures++;
+        } else if (!conflict) {
+            reg_t *e = &g_reg.e[g_reg.n++];
+            e->base = base; e->end = end; e->ulo = fl->ulo; e->uhi = fl->uhi;
+            e->stamp = ++g_reg.clock;
+            e->id = ++g_reg.next_id;
+            e->hold = id ? 1 : 0;
+            if (id) *id = e->id;
+            g_reg.total += end - base;
+        }
     }
-    g_reg.e[g_reg.n].base = base;
-    g_reg.e[g_reg.n].end = end;
-    g_reg.e[g_reg.n].stamp = ++g_reg.clock;
-    g_reg.n++;
-    g_reg.total += end - base;
     reg_span_locked();
     pthread_mutex_unlock(&g_reg.mu);
+    if (hr != hipSuccess) return mvx_buf_kind(p);
+    if (conflict) {
+        reg_unregister(base, dry);
+        return MVX_BUF_PAGEABLE;
+    }
     return MVX_BUF_PINNED;
+}
+
+int mvxi_buf_kind_hold(const void *p, size_t bytes, unsigned long *hold)
+{
+    const int k = mvx_buf_kind(p);                      /* flushes the deferred entries first */
+    if (hold) *hold = 0;
+    if (k == MVX_BUF_DEVICE || !p || !bytes) return k;
+    return reg_range(p, bytes, k, hold);
 }
 
 int mvxi_buf_kind_range(const void *p, size_t bytes)
 {
-    const int k = mvx_buf_kind(p);
-    if (k == MVX_BUF_DEVICE || !p || !bytes) return k;
-    return reg_range(p, bytes, k);
+    return mvxi_buf_kind_hold(p, bytes, NULL);
+}
+
+/* a call's last DMA on the entry is done */
+void mvxi_buf_release(unsigned long hold)
+{
+    int i, done = 0;
+    if (!hold) return;
+    pthread_mutex_lock(&g_reg.mu);
+    for (i = 0; i < g_reg.n && !done; i++)
+        if (g_reg.e[i].id == hold) { g_reg.e[i].hold--; done = 1; }
+    for (i = 0; i < g_reg.nd && !done; i++)
+        if (g_reg.d[i].id == hold) { g_reg.d[i].hold--; done = 1; }
+    pthread_mutex_unlock(&g_reg.mu);
+    reg_flush();
 }
 
 /* explicit registration (dreg_register without a transfer) */
@@ -437,24 +617,28 @@ int mvx_host_register(const void *addr, size_t bytes)
 {
     int on;
     if (!addr || !bytes) return MPI_ERR_ARG;
+    reg_flush();
     pthread_mutex_lock(&g_reg.mu);
     reg_env();
     on = g_reg.on;
     pthread_mutex_unlock(&g_reg.mu);
     if (!on) return MPI_ERR_OTHER;
-    return reg_range(addr, bytes, g_reg.dry ? MVX_BUF_PAGEABLE : mvx_buf_kind(addr)) == MVX_BUF_PINNED
+    return reg_range(addr, bytes, g_reg.dry ? MVX_BUF_PAGEABLE : mvx_buf_kind(addr), NULL) == MVX_BUF_PINNED
                ? MPI_SUCCESS : MPI_ERR_OTHER;
 }
 
 /* ---- release hooks (mpid/ch_gen2/mem_hooks.c:97-132) ------------------------
- * MVAPICH interposes munmap and its own malloc's negative sbrk and drops
+ * MVAPICH interposes munmap and its own malloc's negative sbrk and records
  * every registration inside a released range before the release
  * (find_and_free_dregs_inside, dreg.c:1063).  With glibc's malloc the
  * releases happen inside free() / realloc() (which unmap or trim through
  * libc-internal calls no munmap interposer sees), so libmvx.so interposes
- * those too: free / realloc drop registrations overlapping the block
- * [p, p + malloc_usable_size(p)), munmap / mremap / madvise (DONTNEED, FREE,
- * REMOVE) / negative sbrk the range they release.  Then the real call runs
+ * those too: free / realloc unlink the registrations whose buffers overlap
+ * the block [p, p + malloc_usable_size(p)), munmap / mremap / madvise
+ * (DONTNEED, FREE, REMOVE) / negative sbrk those whose pages overlap the
+ * range they release.  No hook calls into HIP: the unlinked registrations
+ * are unregistered at the next libmvx entry, once no call holds them (the
+ * cache's rules above).  Then the real call runs
  * (the next definition in the lookup order: glibc's, or an allocator
  * interposed after this library).  The hooks take effect when libmvx.so is
  * in the program's global scope ahead of libc -- a program linked with
@@ -488,19 +672,20 @@ __attribute__((constructor)) static void hooks_resolve(void)
     real_sbrk = (void *(*)(intptr_t))dlsym(RTLD_NEXT, "sbrk");
 }
 
-/* cheap test first: no entries, or [lo, hi) outside every entry's span */
-static void hook_release(uintptr_t lo, uintptr_t hi)
+/* cheap test first: no entries, or [lo, hi) outside every entry's span;
+ * nothing while this thread is inside our own (de)registration (dreg.c:1066) */
+static void hook_release(uintptr_t lo, uintptr_t hi, int block)
 {
-    if (!__atomic_load_n(&g_reg_live, __ATOMIC_ACQUIRE) || hi <= lo) return;
+    if (!__atomic_load_n(&g_reg_live, __ATOMIC_ACQUIRE) || hi <= lo || t_in_reg) return;
     if (hi <= __atomic_load_n(&g_reg_lo, __ATOMIC_RELAXED) || lo >= __atomic_load_n(&g_reg_hi, __ATOMIC_RELAXED))
         return;
-    reg_invalidate(lo & ~(PAGE - 1), hi);
+    reg_unlink(lo, hi, block);
 }
 
 static void hook_block(void *p)
 {
     if (p && __atomic_load_n(&g_reg_live, __ATOMIC_ACQUIRE))
-        hook_release((uintptr_t)p, (uintptr_t)p + malloc_usable_size(p));
+        hook_release((uintptr_t)p, (uintptr_t)p + malloc_usable_size(p), 1);
 }
 
 /* the definitions, named so their own addresses can be compared with what
@@ -522,7 +707,7 @@ void *realloc(void *p, size_t n)
 
 static int hook_munmap(void *addr, size_t len)
 {
-    hook_release((uintptr_t)addr, (uintptr_t)addr + len);
+    hook_release((uintptr_t)addr, (uintptr_t)addr + len, 0);
     if (real_munmap) return real_munmap(addr, len);
     return (int)syscall(SYS_munmap, addr, len);
 }
@@ -532,12 +717,12 @@ void *mremap(void *old, size_t old_len, size_t new_len, int flags, ...)
 {
     void *target = NULL;
     va_list ap;
-    hook_release((uintptr_t)old, (uintptr_t)old + old_len);
+    hook_release((uintptr_t)old, (uintptr_t)old + old_len, 0);
     if (flags & MREMAP_FIXED) {
         va_start(ap, flags);
         target = va_arg(ap, void *);
         va_end(ap);
-        hook_release((uintptr_t)target, (uintptr_t)target + new_len);   /* replaced by the move */
+        hook_release((uintptr_t)target, (uintptr_t)target + new_len, 0);   /* replaced by the move */
     }
     if (real_mremap) return real_mremap(old, old_len, new_len, flags, target);
     return (void *)syscall(SYS_mremap, old, old_len, new_len, flags, target);
@@ -546,7 +731,7 @@ void *mremap(void *old, size_t old_len, size_t new_len, int flags, ...)
 int madvise(void *addr, size_t len, int advice)
 {
     if (advice == MADV_DONTNEED || advice == MADV_FREE || advice == MADV_REMOVE)
-        hook_release((uintptr_t)addr, (uintptr_t)addr + len);
+        hook_release((uintptr_t)addr, (uintptr_t)addr + len, 0);
     if (real_madvise) return real_madvise(addr, len, advice);
     return (int)syscall(SYS_madvise, addr, len, advice);
 }
@@ -556,7 +741,7 @@ void *sbrk(intptr_t delta)
     extern void *__sbrk(intptr_t);
     if (delta < 0) {                                   /* mvapich_sbrk */
         const uintptr_t cur = (uintptr_t)(real_sbrk ? real_sbrk(0) : __sbrk(0));
-        hook_release(cur + (uintptr_t)delta, cur);
+        hook_release(cur + (uintptr_t)delta, cur, 0);
     }
     return real_sbrk ? real_sbrk(delta) : __sbrk(delta);
 }

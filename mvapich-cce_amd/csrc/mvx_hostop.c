@@ -98,16 +98,14 @@ static void *host_dev_alias(const void *p)
 }
 
 static int host_apply_locked(MPI_Op op, MPI_Datatype t, const char *in, char *inout, long len,
-                             int in_dev, int io_dev)
+                             int in_dev, int io_dev, int in_pin, int io_pin)
 {
-    int e, ts, rc, bounce_in, bounce_io, in_pin, io_pin;
+    int e, ts, rc, bounce_in, bounce_io;
     long chunk, c, nch, lag;
     size_t bytes, cb, slot;
     hipStream_t sd;
     mvx_dtype_info(t, &e, &ts);
     bytes = (size_t)len * e;
-    in_pin = !in_dev && mvxi_buf_kind_range(in, bytes) == MVX_BUF_PINNED;
-    io_pin = !io_dev && mvxi_buf_kind_range(inout, bytes) == MVX_BUF_PINNED;
     if ((in_dev || in_pin) && (io_dev || io_pin) && zerocopy_on()) {
         const void *din = in_dev ? (const void *)in : host_dev_alias(in);
         void *dio = io_dev ? (void *)inout : host_dev_alias(inout);
@@ -194,13 +192,30 @@ static int host_apply_locked(MPI_Op op, MPI_Datatype t, const char *in, char *in
 
 static pthread_mutex_t g_hop_mu = PTHREAD_MUTEX_INITIALIZER;
 
-/* g_hop's streams and slots serve one call at a time */
+/* g_hop's streams and slots serve one call at a time.  A host operand the
+ * registration cache hands out as page-locked is held until the call's last
+ * DMA on it is done (a failed call drains its streams first). */
 static int host_apply(MPI_Op op, MPI_Datatype t, const char *in, char *inout, long len, int in_dev, int io_dev)
 {
-    int rc;
+    int rc, e, ts;
+    unsigned long hin = 0, hio = 0;
+    size_t bytes;
+    mvx_dtype_info(t, &e, &ts);
+    bytes = (size_t)len * e;
     pthread_mutex_lock(&g_hop_mu);
-    rc = host_apply_locked(op, t, in, inout, len, in_dev, io_dev);
+    {
+        const int in_pin = !in_dev && mvxi_buf_kind_hold(in, bytes, &hin) == MVX_BUF_PINNED;
+        const int io_pin = !io_dev && mvxi_buf_kind_hold(inout, bytes, &hio) == MVX_BUF_PINNED;
+        rc = host_apply_locked(op, t, in, inout, len, in_dev, io_dev, in_pin, io_pin);
+    }
+    if (rc != MPI_SUCCESS && (hin || hio)) {
+        if (g_hop.s[0]) (void)hipStreamSynchronize(g_hop.s[0]);
+        if (g_hop.s[1]) (void)hipStreamSynchronize(g_hop.s[1]);
+        (void)hipGetLastError();
+    }
     pthread_mutex_unlock(&g_hop_mu);
+    mvxi_buf_release(hin);
+    mvxi_buf_release(hio);
     return rc;
 }
 

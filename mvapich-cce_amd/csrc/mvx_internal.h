@@ -49,6 +49,12 @@ int mvx_copy_threads(void);
  * registration cache on a pageable range of at least its minimum is
  * registered (or found registered) and reads as MVX_BUF_PINNED */
 MVXI int mvxi_buf_kind_range(const void *p, size_t bytes);
+/* the same, for a call that will DMA the range: a range the cache hands out
+ * as registered is held for the call (*hold its id, 0 if none) until
+ * mvxi_buf_release(hold) after the call's last DMA on it -- a release of its
+ * memory meanwhile defers the unregistration (mvx_host.c) */
+MVXI int mvxi_buf_kind_hold(const void *p, size_t bytes, unsigned long *hold);
+MVXI void mvxi_buf_release(unsigned long hold);
 MVXI hipError_t mvxi_queue_stream(hipStream_t *s, const char *env, const char *dflt);
 
 /* ---- errors (mvx_comm.c) ----------------------------------------------- */
@@ -130,9 +136,13 @@ typedef struct {
     mvx_xport *t;                    /* nr transports */
     int kinds;                       /* 1: skind / rkind are filled (mvxi_job_kinds) */
     int skind[MVX_MAXP], rkind[MVX_MAXP];   /* MVX_BUF_* of send / recv (empty: DEVICE) */
+    unsigned long shold[MVX_MAXP], rhold[MVX_MAXP];   /* registration holds (mvxi_buf_kind_hold) */
 } job_t;
 
 MVXI int mvxi_job_kinds(job_t *J);
+/* the job is over (rc: its result; on failure the device is drained first,
+ * as copies of a failed pipeline may still be in flight): drop its holds */
+MVXI void mvxi_job_release(job_t *J, int rc);
 MVXI void mvxi_graphs_clear(mvx_comm_t *c);
 MVXI int mvxi_run_device(mvx_comm_t *c, const job_t *J, hipStream_t st);
 MVXI int mvxi_exec_group(rank_exec_t *X, mvx_xport *t, int nr, hipStream_t st, mvx_comm_t *timed);
@@ -177,7 +187,7 @@ MVXI void mvxi_stage_release(stage_res_t *S);
  * buffers, the stream, the staging pool and the variant. */
 #define GRAPH_CACHE 32
 typedef struct {
-    int state;                  /* 0 free, 1 seen once (ran eagerly), 2 captured, 3 retired (mvx_exec.c) */
+    int state;                  /* 0 free, 1 seen once (ran eagerly; mvx_work.seen), 2 captured, 3 retired (mvx_exec.c) */
     unsigned long long hash;
     mvx_plan plan;
     const char *send;
@@ -188,6 +198,7 @@ typedef struct {
     hipGraphExec_t exec;
     int ran_exch;
     int forked;                 /* the graph has parallel branches (graph_forked) */
+    hipEvent_t done;            /* recorded after each launch: the exec is idle once it completes */
     unsigned long stamp;
 } graph_ent_t;
 /* the communicator's staging pool grows to `need` bytes; graphs captured on
@@ -206,7 +217,8 @@ extern __thread int mvxi_capturing MVXI;
 /* The tables one call works in: formerly process statics, now owned by the
  * communicator (allocated at its first call, freed with it). */
 typedef struct mvx_work {
-    graph_ent_t graphs[GRAPH_CACHE];           /* captured device calls */
+    graph_ent_t graphs[GRAPH_CACHE];           /* captured device calls (live or retired) */
+    graph_ent_t seen[GRAPH_CACHE];             /* jobs seen once (ran eagerly), the capture candidates */
     unsigned long graph_clock;
     long graphs_destroyed;                     /* execs destroyed mid-life so far */
     mvx_plan call_plan;                        /* mvx_api.c run(): this rank's plan */

@@ -542,7 +542,17 @@ long mvxi_slice_elems(const mvx_plan *P)
     if (nsl < 2) return 0;
     while (h) { const long t = g % h; g = h; h = t; }      /* gcd(E, 256) */
     m = 256 / g;                                            /* slices start 256-byte aligned */
-    blk = (N + p - 1) / p;
+    /* the longest range the algorithm moves: the whole vector (binomial
+     * Reduce, Scan, recursive doubling, the SMP leader's fold) or a block of
+     * about N / p (Rabenseifner, halving, pairwise); the algorithm is a
+     * function of (coll, count, p, op kind, knobs), the same on every rank */
+    switch (P->alg) {
+    case MVX_ALG_RECDBL: case MVX_ALG_BINOMIAL: case MVX_ALG_SCAN_RECDBL: case MVX_ALG_SMP_LEADER:
+        blk = N;
+        break;
+    default:
+        blk = (N + p - 1) / p;
+    }
     cs = (blk + nsl - 1) / nsl;
     cs = (cs + m - 1) / m * m;
     return cs;
@@ -555,10 +565,15 @@ int mvxi_run_job(mvx_comm_t *c, job_t *J, hipStream_t st, int blocking)
     const int kinds = blocking ? c->call_kinds : MVX_KINDS_UNKNOWN;
     if (J->P[0].packed) return mvxi_run_job_packed(c, J, st, blocking);
     if (kinds != MVX_KINDS_UNKNOWN && J->nr == 1) {
-        /* the caller agreed every rank's kinds (mvx_comm_set_call_kinds) */
+        /* The caller agreed every rank's kinds (mvx_comm_set_call_kinds).
+         * Every rank runs the schedule the hint names, whatever its own
+         * buffers, so a rank whose buffers contradict the hint still pairs
+         * with its peers: under HOST the slices (a device buffer is used in
+         * place), under DEVICE the unsliced device schedule on HBM mirrors
+         * of this rank's host buffers. */
         host = mvxi_job_kinds(J);
-        if (host != (kinds == MVX_KINDS_HOST)) return MPI_ERR_BUFFER;
-        if (host) return mvxi_run_staged(c, J, st);     /* every rank slices alike */
+        if (kinds == MVX_KINDS_HOST) return mvxi_run_staged(c, J, st);
+        if (host) return run_mirrored(c, J, st);
     } else if (blocking && J->nr == 1 && !c->local && (cs = mvxi_slice_elems(&J->P[0])) > 0) {
         mvxi_job_kinds(J);
         return run_staged_cs(c, J, st, cs);

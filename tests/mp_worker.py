@@ -279,8 +279,10 @@ def main():
         # agreed kinds (mvx_comm_set_call_kinds, what the MVAPICH shim passes):
         # every rank device -> the unsliced device path and its exchange
         # variant (PIPE here, reported as such); every rank host -> the
-        # sliced pipeline; a hint the buffers contradict -> MPI_ERR_BUFFER on
-        # every rank (all of them contradict it here), before anything moves
+        # sliced pipeline.  A hint rank 0's buffers contradict: every rank
+        # still runs the schedule the hint names (rank 0's host buffers
+        # through HBM mirrors under DEVICE, its device buffers in place under
+        # HOST), so the transfers pair and the bits are the oracle's
         assert comm.set_exchange(mvx.EXCH_PIPE, 3) == 0
         for op, dtype in [(102, 10), (111, 17)]:
             E = mvx.dtype_info(dtype)[0]
@@ -289,11 +291,10 @@ def main():
                 assert comm.set_call_kinds(kinds) == 0
                 check("ar", dtype, op, n, where, tag="agreed")
                 report.setdefault("agreed_ran", []).append([where, comm.last_exchange()])
-            s_host = np.zeros(n * E, np.uint8)
-            r_host = np.zeros(n * E, np.uint8)
-            assert comm.set_call_kinds(mvx.KINDS_DEVICE) == 0
-            report.setdefault("contradicted", []).append(
-                mvx.MPI_Allreduce(s_host, r_host, n, dtype, op, comm))
+            for kinds, odd, usual in ((mvx.KINDS_DEVICE, "host", "device"), (mvx.KINDS_HOST, "device", "host")):
+                assert comm.set_call_kinds(kinds) == 0
+                check("ar", dtype, op, n, odd if rank == 0 else usual, tag="contradicted")
+                report.setdefault("contradicted", []).append(comm.last_exchange())
         assert comm.set_exchange(mvx.EXCH_P2P, 0) == 0
         del os.environ["MVX_SLICE_MIN_MIB"], os.environ["MVX_SLICE_MIB"]
     else:

@@ -17,6 +17,23 @@
  *                 malloc / free and unrelated mmap / munmap: every
  *                 registration is dropped by its own block's free, exactly
  *                 once, nothing is left, no thread waits on another for good.
+ *   reg_app stub  (built with -DREG_STUB, no GPU): hipHostRegister /
+ *                 hipHostUnregister / hipPointerGetAttributes are counting
+ *                 stubs defined here, so libmvx.so's real (non-dry) cache
+ *                 runs against them: a free of a registered buffer makes no
+ *                 HIP call at all inside the hook -- the registration leaves
+ *                 the cache and waits on the deferred list -- and the next
+ *                 libmvx entry unregisters it (dreg.c:1063-1080, 678-767).
+ *   reg_app neighbour (GPU) a 64 MiB heap buffer pair (not mmap'd: they
+ *                 share their boundary pages with small neighbour blocks)
+ *                 reduced on the device (MPIR_SUM through the registered
+ *                 pages) over and over while a second thread frees and
+ *                 reallocates the neighbour blocks: the registrations stay
+ *                 (no invalidation), every result is bit-exact, no fault.
+ *                 Then the second thread reports a release of the operand
+ *                 itself (mvx_host_invalidate) while a call holds it: the
+ *                 registration is deferred, not unpinned under the DMA, and
+ *                 unregistered once the call is done.
  * Prints "reg_app ok" and one JSON line of what it saw. */
 #define _GNU_SOURCE 1
 #include <malloc.h>
@@ -26,11 +43,43 @@
 #include <stdlib.h>
 #include <string.h>
 #include <sys/mman.h>
+#include <time.h>
 #include <unistd.h>
 
 #include "mvx_coll.h"
 
 #define MIB (1UL << 20)
+
+#ifdef REG_STUB
+/* counting stubs in place of the HIP runtime's (the executable's
+ * definitions come first in the lookup; no GPU needed) */
+#include <hip/hip_runtime_api.h>
+static long n_reg, n_unreg, n_attr;
+static __thread int in_hook_probe;     /* set while a release is in progress on this thread */
+static long hip_in_release;            /* HIP calls made while it was set */
+hipError_t hipHostRegister(void *p, size_t n, unsigned int f)
+{
+    (void)p; (void)n; (void)f;
+    __atomic_add_fetch(&n_reg, 1, __ATOMIC_RELAXED);
+    if (in_hook_probe) __atomic_add_fetch(&hip_in_release, 1, __ATOMIC_RELAXED);
+    return hipSuccess;
+}
+hipError_t hipHostUnregister(void *p)
+{
+    (void)p;
+    __atomic_add_fetch(&n_unreg, 1, __ATOMIC_RELAXED);
+    if (in_hook_probe) __atomic_add_fetch(&hip_in_release, 1, __ATOMIC_RELAXED);
+    return hipSuccess;
+}
+hipError_t hipGetLastError(void) { return hipSuccess; }
+hipError_t hipPointerGetAttributes(hipPointerAttribute_t *a, const void *p)
+{
+    (void)a; (void)p;
+    __atomic_add_fetch(&n_attr, 1, __ATOMIC_RELAXED);
+    if (in_hook_probe) __atomic_add_fetch(&hip_in_release, 1, __ATOMIC_RELAXED);
+    return hipErrorInvalidValue;       /* not HIP memory: pageable */
+}
+#endif
 
 static long entries(void)
 {
@@ -51,6 +100,20 @@ static void *map(size_t n)
 {
     void *p = mmap(NULL, n, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
     return p == MAP_FAILED ? NULL : p;
+}
+
+/* a heap block of `n` bytes and a small block right after it that shares
+ * its last page (retried past the rare layouts where it does not) */
+static int heap_pair(char **a, char **b, size_t n)
+{
+    int t;
+    for (t = 0; t < 8; t++) {
+        *a = malloc(n);
+        *b = malloc(64);
+        if (*a && *b && ((uintptr_t)(*a + n - 1) & ~4095UL) == ((uintptr_t)*b & ~4095UL)) return 0;
+        if (!malloc(48)) return 1;                  /* shift the next pair (kept) */
+    }
+    return 1;
 }
 
 static int dry(void)
@@ -100,9 +163,63 @@ static int dry(void)
     CHECK(mvx_host_register(h, 2 * MIB) == 0 && entries() == 1, "register break");
     CHECK(sbrk(-(intptr_t)(2 * MIB)) != (void *)-1 && entries() == 0, "negative sbrk drops");
 
+    /* heap blocks sharing a page: freeing the neighbour keeps the entry,
+     * freeing the buffer itself drops it */
+    mallopt(M_MMAP_THRESHOLD, 256 * MIB);
+    mallopt(M_TRIM_THRESHOLD, 512 * MIB);
+    CHECK(heap_pair(&a, &b, 4 * MIB) == 0, "neighbour shares a page");
+    CHECK(mvx_host_register(a, 4 * MIB) == 0 && entries() == 1, "register heap block");
+    free(b);
+    CHECK(entries() == 1, "neighbour free keeps");
+    b = malloc(64);
+    free(a);
+    CHECK(entries() == 0, "own free drops");
+    free(b);
+
     printf("{\"mode\": \"dry\", \"invalidations\": %ld}\n", mvx_host_register_invalidations() - inv0);
     return 0;
 }
+
+#ifdef REG_STUB
+static long deferred(void)
+{
+    long d = -1;
+    mvx_host_register_deferred(&d, NULL, NULL);
+    return d;
+}
+
+static int stub(void)
+{
+    char *a, *m;
+    long reg0, unreg0, u0, u1;
+    a = malloc(8 * MIB);
+    memset(a, 1, 8 * MIB);
+    reg0 = n_reg;
+    CHECK(mvx_host_register(a, 8 * MIB) == 0 && entries() == 1 && n_reg == reg0 + 1, "register through the stub");
+    unreg0 = n_unreg;
+    mvx_host_register_deferred(NULL, NULL, &u0);
+    in_hook_probe = 1;
+    free(a);                                        /* the hook: no HIP call */
+    in_hook_probe = 0;
+    CHECK(hip_in_release == 0, "no HIP call inside free()");
+    CHECK(entries() == 0 && deferred() == 1 && n_unreg == unreg0, "free only defers");
+    m = mmap(NULL, 4 * MIB, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    CHECK(m != MAP_FAILED && mvx_host_register(m, 4 * MIB) == 0, "register map");   /* a libmvx entry: flushes */
+    CHECK(n_unreg == unreg0 + 1 && deferred() == 0, "the next entry unregisters the deferred one");
+    in_hook_probe = 1;
+    munmap(m, 4 * MIB);
+    mvx_host_invalidate(m, 4 * MIB);                /* a host MPI's hook: nothing left to drop */
+    in_hook_probe = 0;
+    CHECK(hip_in_release == 0 && deferred() == 1 && n_unreg == unreg0 + 1, "munmap only defers");
+    mvx_host_register_deferred(NULL, NULL, &u1);
+    CHECK(u1 == u0 + 1, "counter agrees");
+    mvx_host_register_enable(0, 0);                 /* off: flushes */
+    CHECK(n_unreg == unreg0 + 2 && deferred() == 0, "off unregisters the rest");
+    printf("{\"mode\": \"stub\", \"registers\": %ld, \"unregisters\": %ld, \"hip_in_release\": %ld}\n",
+           n_reg, n_unreg, hip_in_release);
+    return 0;
+}
+#endif
 
 #define ST_THREADS 8
 #define ST_ITERS 400
@@ -223,6 +340,104 @@ static int gpu(void)
     return 0;
 }
 
+/* ---- neighbour frees and a release under a held registration (GPU) ---- */
+static volatile int nb_stop, nb_go;
+static char *volatile nb_a, *volatile nb_b;
+static long nb_frees;
+static float *nb_inval;
+static size_t nb_bytes;
+static volatile long nb_held_seen = -1;
+
+static void *nb_worker(void *arg)
+{
+    (void)arg;
+    while (!nb_stop) {
+        char *a = nb_a, *b = nb_b;
+        nb_a = NULL; nb_b = NULL;
+        free(a);
+        free(b);
+        nb_a = malloc(64);
+        nb_b = malloc(64);
+        nb_frees += 2;
+    }
+    return NULL;
+}
+
+static void *inval_worker(void *arg)
+{
+    long held = 0;
+    int i;
+    (void)arg;
+    struct timespec t0, t;
+    while (!nb_go) ;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (i = 0; held < 1; i++) {
+        mvx_host_register_deferred(NULL, &held, NULL);
+        clock_gettime(CLOCK_MONOTONIC, &t);
+        if (t.tv_sec - t0.tv_sec > 20) break;
+    }
+    nb_held_seen = held;
+    mvx_host_invalidate(nb_inval, nb_bytes);       /* as a host MPI's hook would */
+    return NULL;
+}
+
+static int neighbour(void)
+{
+    const size_t nb = 64 * MIB, n = nb / sizeof(float);
+    float *x, *y;
+    char *after_x, *after_y;
+    long inv0, hits0, hits1, d0, d1, u0, u1, held_after;
+    int rep, share_x, share_y;
+    pthread_t th;
+    mallopt(M_MMAP_THRESHOLD, 512 * MIB);          /* 64 MiB from the heap, beside other blocks */
+    mallopt(M_TRIM_THRESHOLD, 1024 * MIB);
+    {
+        char *cx, *cy;
+        share_x = heap_pair(&cx, &after_x, nb) == 0;
+        if (!malloc(3 * 4096)) return 1;            /* y's pages apart from x's (else one union entry) */
+        share_y = heap_pair(&cy, &after_y, nb) == 0;
+        x = (float *)cx;
+        y = (float *)cy;
+    }
+    CHECK(share_x && share_y, "the neighbours share the operands' boundary pages");
+    CHECK(sum_check(x, y, n, 3) == 0, "first call");
+    CHECK(entries() == 2, "both operands registered");
+    inv0 = mvx_host_register_invalidations();
+    mvx_host_register_stats(NULL, NULL, &hits0, NULL);
+    nb_a = after_x;
+    nb_b = after_y;
+    CHECK(pthread_create(&th, NULL, nb_worker, NULL) == 0, "thread");
+    for (rep = 0; rep < 24; rep++)
+        CHECK(sum_check(x, y, n, 100 + (unsigned)rep) == 0, "bit-exact while the neighbours churn");
+    nb_stop = 1;
+    pthread_join(th, NULL);
+    mvx_host_register_stats(NULL, NULL, &hits1, NULL);
+    CHECK(mvx_host_register_invalidations() == inv0, "no neighbour free dropped a registration");
+    CHECK(entries() == 2 && hits1 - hits0 == 48, "every call found both registrations");
+
+    /* a release of x itself reported while a call holds it */
+    mvx_host_register_deferred(&d0, NULL, &u0);
+    nb_inval = x;
+    nb_bytes = nb;
+    CHECK(pthread_create(&th, NULL, inval_worker, NULL) == 0, "thread 2");
+    nb_go = 1;
+    CHECK(sum_check(x, y, n, 999) == 0, "bit-exact with the release deferred under it");
+    pthread_join(th, NULL);
+    mvx_host_register_deferred(&d1, &held_after, &u1);
+    CHECK(nb_held_seen >= 1, "the release came while the call held the registration");
+    CHECK(d1 == 0 && held_after == 0 && u1 >= u0 + 1, "unregistered once the call was done");
+    CHECK(entries() == 1, "y stays registered");
+    CHECK(sum_check(x, y, n, 1234) == 0, "the next call registers x again");
+    printf("{\"mode\": \"neighbour\", \"neighbour_frees\": %ld, \"calls\": %d, \"held_seen\": %ld, "
+           "\"unregistered\": %ld}\n", nb_frees, rep, (long)nb_held_seen, u1 - u0);
+    free(nb_a);
+    free(nb_b);
+    free(x);
+    free(y);
+    CHECK(entries() == 0, "frees dropped the registrations");
+    return 0;
+}
+
 int main(int argc, char **argv)
 {
     int rc;
@@ -235,7 +450,12 @@ int main(int argc, char **argv)
         printf("FAIL enable\n");
         return 1;
     }
-    rc = !strcmp(argv[1], "dry") ? dry() : !strcmp(argv[1], "gpu") ? gpu() : !strcmp(argv[1], "stress") ? stress() : 2;
+    rc = !strcmp(argv[1], "dry") ? dry() : !strcmp(argv[1], "gpu") ? gpu() : !strcmp(argv[1], "stress") ? stress()
+       : !strcmp(argv[1], "neighbour") ? neighbour()
+#ifdef REG_STUB
+       : !strcmp(argv[1], "stub") ? stub()
+#endif
+       : 2;
     mvx_host_register_enable(0, 0);
     if (rc == 0) printf("reg_app ok\n");
     return rc;

@@ -18,6 +18,24 @@ Scenarios:
              bit-exact against the oracle, for the four collectives
   fail       as `mixed`; the caller's MVX_DEVICE_ID makes one rank's device
              unusable: every rank returns an error, none hangs
+  kinds_cpu  buffer kinds mixed within a rank (no GPU: the harness is told
+             which host arrays to treat as device memory): every rank
+             reports each call's route agreement -- this rank's ints and the
+             reduced ones -- for the within-rank cases below
+  kinds      the within-rank cases on the GPU (RCCL over its socket
+             transport), bit-exact against the oracle at two sizes (the
+             larger one sliced: MVX_SLICE_MIN_MIB=1 from the test):
+               reduce_dh    device sendbuf everywhere, host recvbuf (the
+                            non-roots' recvbuf is ignored)
+               allreduce_dh device sendbuf, host recvbuf, on every rank
+               rs_hd        rank 0 host sendbuf + device recvbuf, the other
+                            ranks device buffers
+               reduce_dd    device buffers everywhere (non-roots pass a host
+                            recvbuf, which the call never touches)
+  xlate      MVX_HOST_BUFFERS=1 on every rank (from the test), a derived
+             type whose node on rank 1 does not rebuild to the reference's
+             bounds: every rank returns MPI_ERR_TYPE after the one route
+             agreement, without creating the twin
 Writes a JSON report.
 """
 import ctypes
@@ -43,12 +61,14 @@ def main():
     from oracle import oracle as O
     from test_cpu_integration import Nodes, _lib
 
-    gpu = scenario in ("mixed", "fail")
+    gpu = scenario in ("mixed", "fail", "kinds")
     if gpu:
         import importlib
         importlib.import_module("mvapich-cce_amd.transport").rccl_net_env(rank)
     lib = _lib(init=False)
     lib.h_init_world.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_char_p, ctypes.c_double]
+    lib.h_fake_device.argtypes = [ctypes.c_void_p, ctypes.c_long]
+    lib.h_last_route.argtypes = [ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
     assert lib.h_init_world(rank, world, board.encode(), 90.0) == 0
     N = Nodes(lib, O)
     fh, fnode = N.basic(FLOAT)
@@ -56,16 +76,108 @@ def main():
 
     def call(name, fn):
         a0, h0 = lib.h_agree_calls(), lib.h_host_calls()
+        mine, alls = (ctypes.c_int * 3)(), (ctypes.c_int * 3)()
+        r0 = lib.h_last_route(mine, alls)
         t0 = time.time()
         rc = fn()
-        rep["calls"].append({"name": name, "rc": rc, "s": round(time.time() - t0, 3),
-                             "agree": lib.h_agree_calls() - a0, "host": lib.h_host_calls() - h0})
+        rec = {"name": name, "rc": rc, "s": round(time.time() - t0, 3),
+               "agree": lib.h_agree_calls() - a0, "host": lib.h_host_calls() - h0}
+        if lib.h_last_route(mine, alls) != r0:
+            rec["route_mine"], rec["route_all"] = list(mine), list(alls)
+        rep["calls"].append(rec)
         return rc
 
     n = 1000
     sends = [np.arange(n, dtype=np.float32) * (r + 1) + 0.25 * r for r in range(world)]
 
-    if scenario in ("route", "want"):
+    if scenario == "xlate":
+        from test_cpu_integration import DOUBLE
+        i_, d_ = N.basic(INT), N.basic(DOUBLE)
+        oh, good = N.struct([1, 1], [0, 8], [i_, d_])
+        rc_, lb, ub, ext, size = O.type_bounds(oh)
+        node = good if rank != 1 else lib.h_struct(2, (ctypes.c_int * 2)(1, 1), (ctypes.c_long * 2)(0, 8),
+                                                   (ctypes.c_void_p * 2)(i_[1], d_[1]), lb, ub + 8, ext + 8, size)
+        s = np.zeros(n * 16, np.uint8)
+        r = np.zeros(n * 16, np.uint8)
+        call("allreduce_bad_type", lambda: lib.h_allreduce(s.ctypes.data, r.ctypes.data, n, node, MPI_SUM))
+        call("allreduce_good_type", lambda: lib.h_allreduce(s.ctypes.data, r.ctypes.data, n, good, MPI_SUM))
+    elif scenario == "kinds_cpu":
+        root = world - 1
+        cn = (ctypes.c_int * world)(*([n // world] * world))
+
+        def arr(k):
+            return np.zeros(k, np.float32)
+
+        def dev(a):
+            assert lib.h_fake_device(a.ctypes.data, a.nbytes) == 0
+            return a
+        # device sendbuf everywhere, host recvbuf (the non-roots' ignored)
+        s, r = dev(arr(n)), arr(n)
+        call("reduce_dh", lambda: lib.h_reduce(s.ctypes.data, r.ctypes.data, n, fnode, MPI_SUM, root))
+        # device sendbuf + host recvbuf on every rank
+        s2, r2 = dev(arr(n)), arr(n)
+        call("allreduce_dh", lambda: lib.h_allreduce(s2.ctypes.data, r2.ctypes.data, n, fnode, MPI_SUM))
+        # rank 0: host sendbuf + device recvbuf; others device
+        s3 = arr(n) if rank == 0 else dev(arr(n))
+        r3 = dev(arr(n))
+        call("rs_hd", lambda: lib.h_reduce_scatter(s3.ctypes.data, r3.ctypes.data, cn, fnode, MPI_SUM))
+        # device everywhere; the non-roots' host recvbuf is never touched
+        s4 = dev(arr(n))
+        r4 = dev(arr(n)) if rank == root else arr(n)
+        call("reduce_dd", lambda: lib.h_reduce(s4.ctypes.data, r4.ctypes.data, n, fnode, MPI_SUM, root))
+        # device everywhere, Allreduce
+        call("allreduce_dd", lambda: lib.h_allreduce(s4.ctypes.data, r3.ctypes.data, n, fnode, MPI_SUM))
+    elif scenario == "kinds":
+        import torch
+        torch.cuda.set_device(0)
+        root = world - 1
+
+        def mk(a, on_dev):
+            return torch.from_numpy(a.copy()).cuda() if on_dev else a.copy()
+
+        def ptr(b):
+            return b.data_ptr() if isinstance(b, torch.Tensor) else b.ctypes.data
+
+        def host(b):
+            return b.cpu().numpy() if isinstance(b, torch.Tensor) else b
+
+        for size in (1000, 300001):
+            S = [np.arange(size, dtype=np.float32) * (q + 1) + 0.25 * q for q in range(world)]
+            cnts = [size // world + (1 if q < size % world else 0) for q in range(world)]
+            # (name, coll, send on device, recv on device) for this rank
+            cases = [("reduce_dh", COLL_REDUCE, True, False), ("allreduce_dh", COLL_ALLREDUCE, True, False),
+                     ("rs_hd", COLL_REDUCE_SCATTER, rank != 0, True),
+                     ("reduce_dd", COLL_REDUCE, True, rank == root)]
+            for name, coll, sd, rd in cases:
+                nrecv = cnts[rank] if coll == COLL_REDUCE_SCATTER else size
+                s = mk(S[rank], sd)
+                r = mk(np.full(nrecv, -7.0, np.float32), rd)
+                cn = (ctypes.c_int * world)(*cnts)
+                tag = "%s %d" % (name, size)
+                if coll == COLL_ALLREDUCE:
+                    rc = call(tag, lambda: lib.h_allreduce(ptr(s), ptr(r), size, fnode, MPI_SUM))
+                elif coll == COLL_REDUCE:
+                    rc = call(tag, lambda: lib.h_reduce(ptr(s), ptr(r), size, fnode, MPI_SUM, root))
+                else:
+                    rc = call(tag, lambda: lib.h_reduce_scatter(ptr(s), ptr(r), cn, fnode, MPI_SUM))
+                torch.cuda.synchronize()
+                exp = [np.full(cnts[q] if coll == COLL_REDUCE_SCATTER else size, -7.0, np.float32)
+                       for q in range(world)]
+                bs = [x.view(np.uint8) for x in S]
+                be = [x.view(np.uint8) for x in exp]
+                if coll == COLL_ALLREDUCE:
+                    O.allreduce(bs, be, size, FLOAT, MPI_SUM)
+                elif coll == COLL_REDUCE:
+                    O.reduce(bs, be, size, FLOAT, MPI_SUM, root)
+                else:
+                    O.reduce_scatter(bs, be, cnts, FLOAT, MPI_SUM)
+                if coll == COLL_REDUCE and rank != root:
+                    ok = rc == 0
+                else:
+                    ok = rc == 0 and np.array_equal(host(r).view(np.uint32), exp[rank].view(np.uint32))
+                if not ok:
+                    rep["fails"].append({"case": tag, "rc": rc})
+    elif scenario in ("route", "want"):
         s = sends[rank]
         r = np.zeros(n, np.float32)
         cn = (ctypes.c_int * world)(*([n // world] * world))

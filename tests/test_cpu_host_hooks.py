@@ -16,10 +16,12 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 
 
-def _reg_app():
+def _reg_app(stub=False):
+    """stub: the counting HIP stubs of reg_app.c in place of the runtime's"""
     out = os.path.join(tempfile.mkdtemp(prefix="mvx_reg_"), "reg_app")
     pkg = os.path.join(ROOT, "mvapich-cce_amd")
-    subprocess.check_call(["gcc", "-O2", "-std=gnu99", "-Wall", "-Werror", "-D__HIP_PLATFORM_AMD__",
+    extra = ["-DREG_STUB", "-rdynamic"] if stub else []
+    subprocess.check_call(["gcc", "-O2", "-std=gnu99", "-Wall", "-Werror", "-D__HIP_PLATFORM_AMD__"] + extra + [
                            "-I/opt/rocm/include", "-I" + os.path.join(ROOT, "include"),
                            os.path.join(HERE, "reg_app.c"), "-o", out, "-L" + pkg, "-lmvx",
                            "-L/opt/rocm/lib", "-lamdhip64", "-lpthread", "-Wl,-rpath," + pkg, "-Wl,-rpath,/opt/rocm/lib"])
@@ -30,7 +32,20 @@ def test_release_hooks_drop_registrations():
     env = dict(os.environ, MVX_HOST_REGISTER_DRY="1")
     p = subprocess.run([_reg_app(), "dry"], capture_output=True, text=True, timeout=120, env=env)
     assert p.returncode == 0 and "reg_app ok" in p.stdout, p.stdout[-2000:] + p.stderr[-2000:]
-    assert '"invalidations": 7' in p.stdout, p.stdout
+    assert '"invalidations": 8' in p.stdout, p.stdout
+
+
+def test_release_hook_makes_no_hip_call():
+    """The real (non-dry) cache against counting stubs of hipHostRegister /
+    hipHostUnregister / hipPointerGetAttributes / hipGetLastError defined in
+    the program: free() and munmap() of registered memory make no HIP call
+    on the releasing thread -- the registration leaves the cache and waits on
+    the deferred list (dreg.c:1063-1080) -- and the next libmvx entry
+    unregisters it (flush_dereg_mrs_external, dreg.c:678-767)."""
+    p = subprocess.run([_reg_app(stub=True), "stub"], capture_output=True, text=True, timeout=120,
+                       env={k: v for k, v in os.environ.items() if not k.startswith("MVX_HOST_REGISTER")})
+    assert p.returncode == 0 and "reg_app ok" in p.stdout, p.stdout[-2000:] + p.stderr[-2000:]
+    assert '"hip_in_release": 0' in p.stdout and '"unregisters": 2' in p.stdout, p.stdout
 
 
 def test_release_hooks_under_threads():

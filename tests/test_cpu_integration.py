@@ -337,3 +337,45 @@ def test_route_one_rank_wanting_libmvx_takes_every_rank(mvx):
         assert first["s"] < 30, first
         for c in rest:
             assert c["rc"] == 15 and c["host"] == 0 and c["agree"] == 1, c
+
+
+@pytest.mark.parametrize("np_", [2, 3])
+def test_route_kinds_count_only_the_buffers_a_rank_touches(mvx, np_):
+    """Buffer kinds mixed within a rank (the harness treats chosen host
+    arrays as device memory).  The route agreement's second int -- some rank
+    touches host memory -- is 1 whenever any rank's touched buffers include
+    host memory, whichever of its buffers it is: a device sendbuf beside a
+    host recvbuf is host (round 5 reported it as device, and MVX_KINDS_DEVICE
+    then failed that rank alone).  A non-root's Reduce recvbuf is never
+    touched, so a host one there leaves the call all-device.  One route
+    agreement per call (plus the twin's creation agreement at the first,
+    which fails here: no GPU)."""
+    root = np_ - 1
+    for rep in _world(np_, "kinds_cpu"):
+        r = rep["rank"]
+        calls = {c["name"]: c for c in rep["calls"]}
+        want = {"reduce_dh": (r == root, 1), "allreduce_dh": (1, 1), "rs_hd": (r == 0, 1),
+                "reduce_dd": (0, 0), "allreduce_dd": (0, 0)}
+        for name, (mine_host, all_host) in want.items():
+            c = calls[name]
+            assert c["route_mine"][0] == 1, (r, name, c)      # every rank touches a device buffer
+            assert c["route_mine"][1] == int(mine_host), (r, name, c)
+            assert c["route_all"] == [1, all_host, 0], (r, name, c)
+            assert c["rc"] == 15 and c["host"] == 0, (r, name, c)
+            assert c["agree"] == (2 if name == "reduce_dh" else 1), (r, name, c)
+
+
+def test_translation_failure_on_one_rank_fails_every_rank(mvx):
+    """Rank 1's datatype node does not rebuild to the reference's bounds.
+    The shim translates before it agrees the route, so the agreement carries
+    rank 1's MPI_ERR_TYPE: both ranks return it, promptly, after one
+    agreement and without creating the twin (round 5 translated after the
+    agreement: rank 1 failed alone while rank 0 entered the collective).
+    The next call, with a good type everywhere, goes on to the twin."""
+    reps = _world(2, "xlate", {0: {"MVX_HOST_BUFFERS": "1"}, 1: {"MVX_HOST_BUFFERS": "1"}})
+    for rep in reps:
+        bad, good = rep["calls"]
+        assert bad["rc"] == MPI_ERR_TYPE and bad["agree"] == 1 and bad["host"] == 0, (rep["rank"], bad)
+        assert bad["route_all"] == [1, 1, MPI_ERR_TYPE] and bad["s"] < 30, (rep["rank"], bad)
+        assert bad["route_mine"][2] == (MPI_ERR_TYPE if rep["rank"] == 1 else 0), (rep["rank"], bad)
+        assert good["rc"] == 15 and good["agree"] == 2 and good["route_all"] == [1, 1, 0], (rep["rank"], good)

@@ -103,6 +103,29 @@ def test_free_and_reallocate_without_unregister():
     print(p.stdout)
 
 
+def test_neighbour_frees_and_deferred_release_under_dma():
+    """tests/reg_app.c neighbour (cache mode 1, the hooks in effect): two
+    registered 64 MiB heap buffers reduced on the device 24 times while a
+    second thread frees and reallocates the small blocks that share their
+    boundary pages -- no registration is dropped, every result bit-exact, no
+    fault (round 5's hooks unregistered the buffer under the DMA).  Then the
+    second thread reports a release of an operand while a call holds it: the
+    unregistration waits for the call (dreg.c:725-733) and follows it."""
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    out = os.path.join(tempfile.mkdtemp(prefix="mvx_reg_"), "reg_app")
+    pkg = os.path.join(root, "mvapich-cce_amd")
+    subprocess.check_call(["gcc", "-O2", "-std=gnu99", "-Wall", "-Werror", "-D__HIP_PLATFORM_AMD__",
+                           "-I/opt/rocm/include", "-I" + os.path.join(root, "include"),
+                           os.path.join(here, "reg_app.c"), "-o", out, "-L" + pkg, "-lmvx",
+                           "-L/opt/rocm/lib", "-lamdhip64", "-lpthread", "-Wl,-rpath," + pkg,
+                           "-Wl,-rpath,/opt/rocm/lib"])
+    env = {k: v for k, v in os.environ.items() if not k.startswith("MVX_HOST_REGISTER")}
+    p = subprocess.run([out, "neighbour"], capture_output=True, text=True, timeout=180, env=env)
+    assert p.returncode == 0 and "reg_app ok" in p.stdout, p.stdout[-2000:] + p.stderr[-2000:]
+    print(p.stdout)
+
+
 def test_free_and_reallocate_same_size(mvx):
     """Mode 2 (this process's contract): a registered buffer is
     unregistered, freed and the same size allocated again (the same address

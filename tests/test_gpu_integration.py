@@ -162,3 +162,26 @@ def test_twin_creation_failure_on_one_rank_fails_every_rank(mvx):
         assert len(rep["calls"]) == 4
         for c in rep["calls"]:
             assert c["rc"] == 15 and c["host"] == 0 and c["s"] < 30, (rep["rank"], c)
+
+
+@pytest.mark.parametrize("np_", [2, 3])
+def test_within_rank_kinds_through_the_shim(mvx, np_):
+    """Buffer kinds mixed within a rank (round 5's regression: a rank with a
+    device sendbuf and a host recvbuf was counted as device, the shim passed
+    MVX_KINDS_DEVICE, and that rank failed alone while its peers waited in
+    RCCL):
+      Reduce with device sendbufs everywhere and a host recvbuf at the root;
+      Allreduce with device send and host recv on every rank;
+      Reduce_scatter with host send and device recv on rank 0 only;
+      Reduce with device buffers everywhere (the non-roots' host recvbuf is
+      never touched: the call is agreed all-device).
+    Every rank's recvbuf is the oracle's replay bit for bit, at 1000 and
+    300001 floats (the larger one in slices: MVX_SLICE_MIN_MIB=1)."""
+    env = {"MVX_SLICE_MIN_MIB": "1", "MVX_SLICE_MIB": "1"}
+    for rep in _world(np_, "kinds", {r: env for r in range(np_)}, timeout=300):
+        assert not rep["fails"], rep
+        assert len(rep["calls"]) == 8
+        for c in rep["calls"]:
+            assert c["rc"] == 0 and c["host"] == 0 and c["agree"] in (1, 3), c
+        dd = [c for c in rep["calls"] if c["name"].startswith("reduce_dd")]
+        assert all(c["route_all"][1] == 0 for c in dd), dd        # agreed all-device

@@ -308,3 +308,50 @@ def test_random_derived_sweep(mvx, oracle, types, batch):
         for c in comms.values():
             c.free()
         assert mvx.MPI_Type_free(types["hidx_neg"])[0] == 0 and oracle.type_free(types["hidx_neg"]) == 0
+
+
+def test_whole_word_unpack_keeps_every_other_byte(mvx, oracle):
+    """Unpack of types whose maps leave holes inside 64-byte sectors runs by
+    whole 16-byte words (mvx_dtype.hip k_unpack_merge: each tile read into
+    LDS, the units merged in, written back whole).  Against the oracle's
+    type-map copy over a patterned buffer with guard bands: type-map bytes
+    land, holes and guards keep their pattern -- at counts 1, 2, 3, 1000
+    and 100003, with the origin at every 4-byte phase of a 16-byte word (the
+    first and last words of the hull are partial there and take unit stores
+    instead), and for a type reaching below its origin (negative stride)."""
+    import torch
+    made = [
+        _both(mvx, oracle, "vector", 8, 1, 4, D),              # 8 B of every 32
+        _both(mvx, oracle, "vector", 2, 1, 2, F),              # every other float
+        _both(mvx, oracle, "struct", 2, [1, 1], [0, 8], [I, D]),  # {int; hole; double}
+        _both(mvx, oracle, "hvector", 3, 1, -20, I),           # reaches below the origin
+        _both(mvx, oracle, "hindexed", 3, [1, 2, 1], [0, 12, 40], F),
+    ]
+    try:
+        for h in made:
+            ext = mvx.MPI_Type_extent(h)[1]
+            size = mvx.MPI_Type_size(h)[1]
+            L = mvx.type_layout(h)
+            for n in (1, 2, 3, 1000, 100003):
+                for phase in (0, 4, 8, 12):
+                    guard = 256
+                    off = guard + phase - min(0, L["span_lo"])
+                    nb = off + (n - 1) * ext + L["span_hi"] + guard
+                    rng = np.random.default_rng(n * 7 + phase + h)
+                    x = np.zeros(nb, np.uint8)
+                    x[off + min(0, L["span_lo"]):nb - guard] = rng.integers(
+                        0, 256, nb - guard - off - min(0, L["span_lo"]), dtype=np.uint8)
+                    y0 = rng.integers(0, 256, nb, dtype=np.uint8)
+                    dx = torch.from_numpy(x).cuda()
+                    dy = torch.from_numpy(y0).cuda()
+                    dp = torch.zeros(max(n * size, 16), dtype=torch.uint8, device="cuda")
+                    assert mvx.type_pack(h, dx.data_ptr() + off, dp, n) == 0
+                    assert mvx.type_unpack(h, dp, dy.data_ptr() + off, n) == 0
+                    ref = y0.copy()
+                    assert oracle.type_copy(ref[off:], x[off:], n, h) == 0
+                    got = T.from_dev(dy)
+                    assert np.array_equal(got, ref), (h, n, phase, np.flatnonzero(got != ref)[:8])
+    finally:
+        for h in made:
+            mvx.MPI_Type_free(h)
+            oracle.type_free(h)

@@ -90,9 +90,18 @@ def main():
                    "packed_bytes": n * size, "us": round(us, 2),
                    "alg_GBs": round(alg / (us * 1e-6) / 1e9, 1), "alg_frac": round(alg / (us * 1e-6) / 1e9 / PEAK, 4)}
             if touched is not None:
-                lb = touched + n * size          # lines of the span read (pack) or read + written (unpack: RMW)
+                lb = touched + n * size          # lines of the span read (pack) or written (unpack)
                 out["line_GBs"] = round(lb / (us * 1e-6) / 1e9, 1)
                 out["line_frac"] = round(lb / (us * 1e-6) / 1e9 / PEAK, 4)
+                if direction == "unpack":
+                    # what DRAM moves when the hole bytes of partly written
+                    # lines must be kept: every touched line read and written
+                    # (by the memory on a byte-masked store, by the kernel in
+                    # MVX_UNPACK_MERGE's whole-word unpack)
+                    rmw = 2 * touched + n * size
+                    out["rmw_GBs"] = round(rmw / (us * 1e-6) / 1e9, 1)
+                    out["rmw_frac"] = round(rmw / (us * 1e-6) / 1e9 / PEAK, 4)
+            out["merge"] = os.environ.get("MVX_UNPACK_MERGE", "1") != "0"
             print(json.dumps(out), flush=True)
         del sets
         torch.cuda.empty_cache()
