@@ -661,10 +661,21 @@ static int launch_units(const Type &t, int wi, const void *src, void *dst, long 
 #define MERGE_TILE 8192              // destination bytes per workgroup (LDS)
 #define MERGE_UNITS_LDS 2048
 
+template <int W> __device__ inline typename UnitT<W>::t unit_of(const pu32x4 &v, int g);
+template <> __device__ inline uint32_t unit_of<4>(const pu32x4 &v, int g) { return v[g]; }
+template <> __device__ inline pu32x2 unit_of<8>(const pu32x4 &v, int g)
+{
+    pu32x2 r;
+    r.x = v[2 * g];
+    r.y = v[2 * g + 1];
+    return r;
+}
+template <> __device__ inline pu32x4 unit_of<16>(const pu32x4 &v, int) { return v; }
+
 template <int W>
 __global__ void __launch_bounds__(256)
 k_unpack_merge(const char *__restrict__ packed, char *__restrict__ dst, const int *__restrict__ uoff, long upe,
-               long n, long ext, long lo, long hi, uintptr_t a0, uintptr_t h0, uintptr_t h1, long D, long R)
+               long n, long ext, long lo, long hi, uintptr_t a0, uintptr_t h0, uintptr_t h1)
 {
     typedef typename UnitT<W>::t V;
     __shared__ pu32x4 s_tile[MERGE_TILE / 16];
@@ -684,20 +695,38 @@ k_unpack_merge(const char *__restrict__ packed, char *__restrict__ dst, const in
     long ilo = a - hi >= 0 ? (a - hi) / ext + 1 : 0;
     long ihi = b - lo > 0 ? (b - lo + ext - 1) / ext : 0;
     if (ihi > n) ihi = n;
-    const long qend = ihi * upe;
-    long q = ilo * upe + threadIdx.x;
-    long i = q / upe, j = q - i * upe;
-    for (; q < qend; q += 256) {
-        const long off = i * ext + (lds_units ? s_uoff[j] : uoff[j]);
-        if (off >= a && off < b) {
-            const V v = __builtin_nontemporal_load((const V *)(packed + q * W));
-            const uintptr_t at = (uintptr_t)dst + off, word = at & ~(uintptr_t)15;
-            if (word < h0 || word + 16 > h1) *(V *)at = v;                    // a word past the hull: its units only
-            else *(V *)((char *)s_tile + (at - t0)) = v;
+    // the units of those elements, read 16 bytes of the packed stream (G
+    // units) per lane, two chunks in flight; a chunk that runs past the
+    // stream's end is read unit by unit
+    constexpr int G = 16 / W;
+    const long qn = n * upe, c0 = ilo * upe / G, c1 = (ihi * upe + G - 1) / G;
+    for (long c = c0 + threadIdx.x; c < c1; c += 512) {
+        pu32x4 v[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const long cc = c + 256 * u;
+            if (cc < c1 && (cc + 1) * G <= qn) v[u] = __builtin_nontemporal_load((const pu32x4 *)(packed + 16 * cc));
         }
-        i += D;
-        j += R;
-        if (j >= upe) { j -= upe; i++; }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const long cc = c + 256 * u;
+            if (cc >= c1) continue;
+            const bool whole = (cc + 1) * G <= qn;
+            long q = cc * G, i = q / upe, j = q - i * upe;
+#pragma unroll
+            for (int g = 0; g < G; ++g, ++q) {
+                if (q < qn) {
+                    const long off = i * ext + (lds_units ? s_uoff[j] : uoff[j]);
+                    if (off >= a && off < b) {
+                        const V x = whole ? unit_of<W>(v[u], g) : *(const V *)(packed + q * W);
+                        const uintptr_t at = (uintptr_t)dst + off, word = at & ~(uintptr_t)15;
+                        if (word < h0 || word + 16 > h1) *(V *)at = x;        // a word past the hull: its units only
+                        else *(V *)((char *)s_tile + (at - t0)) = x;
+                    }
+                }
+                if (++j == upe) { j = 0; ++i; }
+            }
+        }
     }
     __syncthreads();
     for (int w = threadIdx.x; w < nw; w += 256) {
@@ -765,7 +794,7 @@ static int launch_merge(Type &t, int wi, const void *src, void *dst, long count,
     const long tiles = (long)((((h1 + 15) & ~(uintptr_t)15) - a0 + MERGE_TILE - 1) / MERGE_TILE);
     if (tiles < 1 || tiles > INT32_MAX) return MPI_ERR_OTHER;
     hipLaunchKernelGGL((k_unpack_merge<W>), dim3((unsigned)tiles), dim3(256), 0, st, (const char *)src, (char *)dst,
-                       (const int *)t.dunits[wi], upe, count, t.extent, lo, hi, a0, h0, h1, 256 / upe, 256 % upe);
+                       (const int *)t.dunits[wi], upe, count, t.extent, lo, hi, a0, h0, h1);
     return hipGetLastError() == hipSuccess ? MPI_SUCCESS : MPI_ERR_OTHER;
 }
 
@@ -813,7 +842,7 @@ static int pack(int h, const void *src, void *dst, size_t count, hipStream_t st,
         for (int wi = 0; units_on && wi < 3; ++wi) {
             const int W = Ws[wi];
             if (al % W || !unit_table(*t, W, wi)) continue;
-            if (!packing && merge_on()) {
+            if (!packing && merge_on() && (uintptr_t)src % 16 == 0) {
                 if (!t->merge) t->merge = merge_ok(*t, &t->mlo, &t->mhi) ? 1 : -1;
                 if (t->merge > 0) {
                     if (W == 16) return launch_merge<16>(*t, wi, src, dst, (long)count, t->mlo, t->mhi, st);

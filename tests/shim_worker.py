@@ -32,6 +32,9 @@ Scenarios:
                             ranks device buffers
                reduce_dd    device buffers everywhere (non-roots pass a host
                             recvbuf, which the call never touches)
+  latency    an 8-byte device Allreduce (two floats) 300 times with the route
+             agreed and 300 times under MVX_SHIM_ROUTE=local (no agreement),
+             interleaved in blocks; reports each mode's median call time
   xlate      MVX_HOST_BUFFERS=1 on every rank (from the test), a derived
              type whose node on rank 1 does not rebuild to the reference's
              bounds: every rank returns MPI_ERR_TYPE after the one route
@@ -61,7 +64,7 @@ def main():
     from oracle import oracle as O
     from test_cpu_integration import Nodes, _lib
 
-    gpu = scenario in ("mixed", "fail", "kinds")
+    gpu = scenario in ("mixed", "fail", "kinds", "latency")
     if gpu:
         import importlib
         importlib.import_module("mvapich-cce_amd.transport").rccl_net_env(rank)
@@ -127,6 +130,27 @@ def main():
         call("reduce_dd", lambda: lib.h_reduce(s4.ctypes.data, r4.ctypes.data, n, fnode, MPI_SUM, root))
         # device everywhere, Allreduce
         call("allreduce_dd", lambda: lib.h_allreduce(s4.ctypes.data, r3.ctypes.data, n, fnode, MPI_SUM))
+    elif scenario == "latency":
+        import torch
+        torch.cuda.set_device(0)
+        ds = torch.ones(2, dtype=torch.float32, device="cuda")
+        dr = torch.zeros(2, dtype=torch.float32, device="cuda")
+        times = {"agree": [], "local": []}
+        for blk in range(12):
+            for mode in ("agree", "local"):
+                if mode == "local":
+                    os.environ["MVX_SHIM_ROUTE"] = "local"
+                for _ in range(25):
+                    t0 = time.perf_counter()
+                    rc = lib.h_allreduce(ds.data_ptr(), dr.data_ptr(), 2, fnode, MPI_SUM)
+                    times[mode].append(time.perf_counter() - t0)
+                    if rc:
+                        rep["fails"].append({"case": "latency " + mode, "rc": rc})
+                os.environ.pop("MVX_SHIM_ROUTE", None)
+        if blk == 11 and float(dr[0]) != world:
+            rep["fails"].append({"case": "latency value", "got": float(dr[0])})
+        times = {k: sorted(v[5:]) for k, v in times.items()}      # the first calls create the twin
+        rep["latency_us"] = {k: round(1e6 * v[len(v) // 2], 1) for k, v in times.items()}
     elif scenario == "kinds":
         import torch
         torch.cuda.set_device(0)

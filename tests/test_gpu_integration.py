@@ -185,3 +185,14 @@ def test_within_rank_kinds_through_the_shim(mvx, np_):
             assert c["rc"] == 0 and c["host"] == 0 and c["agree"] in (1, 3), c
         dd = [c for c in rep["calls"] if c["name"].startswith("reduce_dd")]
         assert all(c["route_all"][1] == 0 for c in dd), dd        # agreed all-device
+
+
+def test_route_agreement_latency(mvx):
+    """The per-call route agreement's cost: an 8-byte device
+    Allreduce at p = 2 through the shim, agreed vs MVX_SHIM_ROUTE=local, the
+    agreement over the harness's host transport (a shared-memory board).
+    Both modes must return the right sum; the medians are reported."""
+    reps = _world(2, "latency", timeout=300)
+    for rep in reps:
+        assert not rep["fails"], rep
+        print("rank", rep["rank"], "median us per call", rep["latency_us"])
