@@ -84,7 +84,7 @@ def parse(argv=None):
     ap.add_argument("--prewarm-ms", type=float, default=0.0,
                     help="N = 1: untimed back-to-back steps for this long before the W warmup steps "
                          "(0 = none); reported in the line")
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r05", "pmc_c2.json"),
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r06", "pmc_c2.json"),
                     help="committed rocprofv3 PMC summary for the traffic field")
     ap.add_argument("--block-cap", type=int, default=0)
     ap.add_argument("--nt-min-log2", type=int, default=0, help="-1 disables non-temporal loads/stores")
