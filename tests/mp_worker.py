@@ -70,11 +70,13 @@ def main():
         tot = sum(cnts) if cnts else n_or_cnts
         S = inputs(dtype, tot, fill)
         nrecv = cnts[rank] if cnts else tot
-        if where == "device":
-            s = T.to_dev(S[rank])
+        # where: "device" / "host" for both buffers, "dh" device sendbuf +
+        # host recvbuf, "hd" the other way round (kinds mixed within a rank)
+        sdev, rdev = where in ("device", "dh"), where in ("device", "hd")
+        s = T.to_dev(S[rank]) if sdev else T.clone(S[rank]).view(np.uint8)
+        if rdev:
             r = torch.zeros(max(nrecv, 1) * E, dtype=torch.uint8, device="cuda")
         else:
-            s = T.clone(S[rank]).view(np.uint8)
             r = np.zeros(max(nrecv, 1) * E, np.uint8)
         if coll == "ar":
             rc = mvx.MPI_Allreduce(s, r, tot, dtype, op, comm)
@@ -145,7 +147,7 @@ def main():
             E = mvx.dtype_info(dtype)[0]
             n = int(rng.choice([1, 7, 255, 4097, 70001, 300007]))
             n = min(n, (16 << 20) // E // world)
-            where = str(rng.choice(["device", "host"]))
+            where = str(rng.choice(["device", "host", "dh", "hd"]))
             root = int(rng.integers(0, world))
             if coll == "rs":
                 check(coll, dtype, op, [max(0, n // world + int(rng.integers(-2, 3))) for _ in range(world)], where,
@@ -231,26 +233,26 @@ def main():
         report["graph_stats"] = comm.graph_stats()
         comm.set_graphs(False)
     elif suite == "mixed":
-        # buffer kinds differing between the ranks of one call (MPI allows
-        # it): rank r passes host buffers when (case + r) is even, device
-        # buffers otherwise -- host calls run on HBM mirrors and move what a
+        # buffer kinds differing between the ranks of one call and between a
+        # rank's two buffers (MPI allows both): rank r's kinds rotate through
+        # host, device, device send + host recv, host send + device recv with
+        # (case + r) -- host buffers run on HBM mirrors and move what a
         # device call moves, so the transfers pair up
         case = 0
+        kinds = ("host", "device", "dh", "hd")
         for name, mode, sl in modes:
             assert comm.set_exchange(mode, sl) == 0
             for op, dtype in [(102, 10), (111, 17), (105, 8), (103, 6)]:
                 for n in (10, 70001, 300000, 4096 * world * 4):
-                    check("ar", dtype, op, n, "host" if (case + rank) % 2 == 0 else "device", tag=name)
+                    check("ar", dtype, op, n, kinds[(case + rank) % 4], tag=name)
                     case += 1
                 for n in (5, 70001):
-                    check("red", dtype, op, n, "host" if (case + rank) % 2 == 0 else "device", root=world - 1,
-                          tag=name)
+                    check("red", dtype, op, n, kinds[(case + rank) % 4], root=world - 1, tag=name)
                     case += 1
                 for base in (3, 140000):
-                    check("rs", dtype, op, [base] * world, "host" if (case + rank) % 2 == 0 else "device",
-                          tag=name)
+                    check("rs", dtype, op, [base] * world, kinds[(case + rank) % 4], tag=name)
                     case += 1
-                check("scan", dtype, op, 5000, "host" if (case + rank) % 2 == 0 else "device", tag=name)
+                check("scan", dtype, op, 5000, kinds[(case + rank) % 4], tag=name)
                 case += 1
     elif suite == "sliced":
         # the slice schedule (mvx_stage.c: blocking calls at p > 1 from
@@ -265,7 +267,7 @@ def main():
             E = mvx.dtype_info(dtype)[0]
             for how in ("mixed", "host", "device"):
                 def where():
-                    return how if how != "mixed" else ("host" if (case + rank) % 2 == 0 else "device")
+                    return how if how != "mixed" else ("host", "device", "dh", "hd")[(case + rank) % 4]
                 for n in ((1 << 20) // E + 1, (3 << 20) // E + 7):
                     check("ar", dtype, op, n, where(), tag="sliced")
                     case += 1
