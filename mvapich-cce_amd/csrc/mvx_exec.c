@@ -630,9 +630,9 @@ static int graph_forked(hipGraph_t g)
 }
 
 /* The pool is about to be freed: every graph captured on it goes first --
- * destroyed where the runtime allows it (after the device drained, so no
- * launch of it is in flight), else retired (kept, never matched again,
- * destroyed with the communicator). */
+ * destroyed where the runtime allows it (after its own last launch
+ * completed, so none of it is in flight), else retired (kept, never matched
+ * again, destroyed with the communicator). */
 int mvxi_grow_pool(mvx_comm_t *c, size_t need)
 {
     int i;
@@ -646,10 +646,13 @@ int mvxi_grow_pool(mvx_comm_t *c, size_t need)
             if (g->state == G_LIVE) { g->state = G_RETIRED; gone += graph_evictable(c, g); }
         }
         if (gone) {
-            hipDeviceSynchronize();
-            for (i = 0; i < GRAPH_CACHE; i++)
-                if (c->w->graphs[i].state == G_RETIRED && graph_evictable(c, &c->w->graphs[i]))
-                    graph_evict(c, &c->w->graphs[i]);
+            for (i = 0; i < GRAPH_CACHE; i++) {
+                graph_ent_t *g = &c->w->graphs[i];
+                if (g->state != G_RETIRED || !graph_evictable(c, g)) continue;
+                /* its last launch done (the pool it reads is about to go) */
+                if (g->done && hipEventSynchronize(g->done) != hipSuccess) (void)hipGetLastError();
+                graph_evict(c, g);
+            }
         }
     }
     return mvxi_grow(&c->pool, &c->pool_bytes, need);
