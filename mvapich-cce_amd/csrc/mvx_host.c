@@ -237,7 +237,10 @@ int mvx_copy_threads(void)
  * (and pinned) for as long as the buffer lives. */
 
 #define REG_MAX 64
-#define REG_DEFER (2 * REG_MAX)    /* new entries are refused while REG_MAX are deferred */
+/* new entries are refused while REG_MAX are deferred (checked at the insert
+ * itself), so the table and the deferred list never hold more than
+ * 2 * REG_MAX - 1 between them: every deferral moves a table entry */
+#define REG_DEFER (2 * REG_MAX)
 #define REG_FLY 8                  /* registrations in progress (hipHostRegister outside the lock) */
 #define PAGE 4096UL
 typedef struct { uintptr_t base, end, ulo, uhi; unsigned long stamp, id; int hold; } reg_t;
@@ -560,7 +563,8 @@ static int reg_range(const void *p, size_t bytes, int k, unsigned long *id)
         reg_fly_t *fl = &g_reg.fly[f];
         /* meanwhile: a release of these pages (stale), another entry over
          * them, or the table / the byte budget filled */
-        conflict = fl->stale || g_reg.n == REG_MAX || g_reg.total + (end - base) > g_reg.max_bytes;
+        conflict = fl->stale || g_reg.n == REG_MAX || g_reg.nd >= REG_MAX ||
+                   g_reg.total + (end - base) > g_reg.max_bytes;
         for (i = 0; !conflict && i < g_reg.n; i++) conflict = overlaps(g_reg.e[i].base, g_reg.e[i].end, base, end);
         fl->used = 0;
         if (hr != hipSuccess) {
