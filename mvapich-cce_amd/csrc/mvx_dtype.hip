@@ -672,19 +672,19 @@ template <> __device__ inline pu32x2 unit_of<8>(const pu32x4 &v, int g)
 }
 template <> __device__ inline pu32x4 unit_of<16>(const pu32x4 &v, int) { return v; }
 
-template <int W>
+template <int W, int TILE>
 __global__ void __launch_bounds__(256)
 k_unpack_merge(const char *__restrict__ packed, char *__restrict__ dst, const int *__restrict__ uoff, long upe,
                long n, long ext, long lo, long hi, uintptr_t a0, uintptr_t h0, uintptr_t h1)
 {
     typedef typename UnitT<W>::t V;
-    __shared__ pu32x4 s_tile[MERGE_TILE / 16];
+    __shared__ pu32x4 s_tile[TILE / 16];
     __shared__ int s_uoff[MERGE_UNITS_LDS];
     const bool lds_units = upe <= MERGE_UNITS_LDS;
     if (lds_units)
         for (int u = threadIdx.x; u < (int)upe; u += 256) s_uoff[u] = uoff[u];
-    const uintptr_t t0 = a0 + (uintptr_t)blockIdx.x * MERGE_TILE;          // this tile's first word
-    const uintptr_t tend = t0 + MERGE_TILE < ((h1 + 15) & ~(uintptr_t)15) ? t0 + MERGE_TILE
+    const uintptr_t t0 = a0 + (uintptr_t)blockIdx.x * TILE;                // this tile's first word
+    const uintptr_t tend = t0 + TILE < ((h1 + 15) & ~(uintptr_t)15) ? t0 + TILE
                                                                            : ((h1 + 15) & ~(uintptr_t)15);
     const int nw = (int)((tend - t0) / 16);
     for (int w = threadIdx.x; w < nw; w += 256)
@@ -791,10 +791,139 @@ static int launch_merge(Type &t, int wi, const void *src, void *dst, long count,
     const long upe = t.units[wi];
     const uintptr_t h0 = (uintptr_t)dst + lo, h1 = (uintptr_t)dst + (count - 1) * t.extent + hi;
     const uintptr_t a0 = h0 & ~(uintptr_t)15;
-    const long tiles = (long)((((h1 + 15) & ~(uintptr_t)15) - a0 + MERGE_TILE - 1) / MERGE_TILE);
+    // MVX_UNPACK_TILE_KIB: 8 (default) or 16 (tuning; 4 KiB ran 30-40 %
+    // slower, 16 within a few per cent either way, profiles/r06/pack_tile_sizes.txt)
+    static long TILE = 0;
+    if (!TILE) {
+        const char *e = getenv("MVX_UNPACK_TILE_KIB");
+        TILE = e && atoi(e) == 16 ? 16384 : MERGE_TILE;
+    }
+    const long tiles = (long)((((h1 + 15) & ~(uintptr_t)15) - a0 + TILE - 1) / TILE);
     if (tiles < 1 || tiles > INT32_MAX) return MPI_ERR_OTHER;
-    hipLaunchKernelGGL((k_unpack_merge<W>), dim3((unsigned)tiles), dim3(256), 0, st, (const char *)src, (char *)dst,
-                       (const int *)t.dunits[wi], upe, count, t.extent, lo, hi, a0, h0, h1);
+    if (TILE == 16384)
+        hipLaunchKernelGGL((k_unpack_merge<W, 16384>), dim3((unsigned)tiles), dim3(256), 0, st, (const char *)src,
+                           (char *)dst, (const int *)t.dunits[wi], upe, count, t.extent, lo, hi, a0, h0, h1);
+    else
+        hipLaunchKernelGGL((k_unpack_merge<W, MERGE_TILE>), dim3((unsigned)tiles), dim3(256), 0, st,
+                           (const char *)src, (char *)dst, (const int *)t.dunits[wi], upe, count, t.extent, lo, hi,
+                           a0, h0, h1);
+    return hipGetLastError() == hipSuccess ? MPI_SUCCESS : MPI_ERR_OTHER;
+}
+
+// ---- pack by whole words ----------------------------------------------------
+// The unit kernel's pack reads 4 or 8 bytes per lane from the extent layout
+// and writes as many to the packed stream: four or two times the memory
+// instructions of 16-byte accesses, with each read instruction spread over
+// several lines.  This variant gives a workgroup a run of whole elements:
+// it loads their hull into LDS with 16-byte loads (whole aligned words: a
+// word holding one hull byte lies in the same page, so the read is safe),
+// then each lane gathers G = 16 / W units from LDS into one 16-byte chunk of
+// the packed stream and stores it whole.  A run's packed bytes start on a
+// 16-byte boundary (its element count is a multiple of 16 / gcd(size, 16));
+// the stream's last, partial chunk is stored unit by unit.
+#define PACK_TILE 8192               // LDS bytes of extent layout per workgroup
+
+template <int W, int TILE>
+__global__ void __launch_bounds__(256)
+k_pack_tiles(const char *__restrict__ src, char *__restrict__ dst, const int *__restrict__ uoff, long upe, long n,
+             long ext, long lo, long hi, long ept)
+{
+    typedef typename UnitT<W>::t V;
+    constexpr int G = 16 / W;
+    __shared__ pu32x4 s_tile[TILE / 16];
+    __shared__ int s_uoff[MERGE_UNITS_LDS];
+    const bool lds_units = upe <= MERGE_UNITS_LDS;
+    if (lds_units)
+        for (int u = threadIdx.x; u < (int)upe; u += 256) s_uoff[u] = uoff[u];
+    const long i0 = (long)blockIdx.x * ept;
+    const long i1 = i0 + ept < n ? i0 + ept : n;
+    const uintptr_t a0 = ((uintptr_t)src + i0 * ext + lo) & ~(uintptr_t)15;
+    const uintptr_t a1 = ((uintptr_t)src + (i1 - 1) * ext + hi + 15) & ~(uintptr_t)15;
+    const int nw = (int)((a1 - a0) / 16);
+    for (int w = threadIdx.x; w < nw; w += 256)
+        s_tile[w] = __builtin_nontemporal_load((const pu32x4 *)(a0 + 16 * (uintptr_t)w));
+    __syncthreads();
+    const long qn = n * upe, qlo = i0 * upe, qhi = i1 * upe;
+    const long c0 = qlo / G, c1 = (qhi + G - 1) / G;      // qlo is a multiple of G (ept)
+    const long base = (long)(a0 - (uintptr_t)src);          // the tile's offset from src
+    for (long c = c0 + threadIdx.x; c < c1; c += 256) {
+        long q = c * G, i = q / upe, j = q - i * upe;
+        if ((c + 1) * G <= qn) {
+            pu32x4 out;
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                const long off = i * ext + (lds_units ? s_uoff[j] : uoff[j]) - base;
+                const V x = *(const V *)((const char *)s_tile + off);
+                if constexpr (W == 4) out[g] = x;
+                else { out[2 * g] = x.x; out[2 * g + 1] = x.y; }
+                if (++j == upe) { j = 0; ++i; }
+            }
+            __builtin_nontemporal_store(out, (pu32x4 *)(dst + 16 * c));
+        } else {
+            for (int g = 0; g < G && q < qn; ++g, ++q) {
+                const long off = i * ext + (lds_units ? s_uoff[j] : uoff[j]) - base;
+                *(V *)(dst + q * W) = *(const V *)((const char *)s_tile + off);
+                if (++j == upe) { j = 0; ++i; }
+            }
+        }
+    }
+}
+
+// MVX_PACK_TILES: 1 (default) pack maps of 4- and 8-byte units through LDS
+// tiles where an element's hull is small, 0 the unit kernel everywhere
+static int tiles_on()
+{
+    static int on = -1;
+    if (on < 0) {
+        const char *e = getenv("MVX_PACK_TILES");
+        on = e ? atoi(e) != 0 : 1;
+    }
+    return on;
+}
+
+// MVX_PACK_TILE_KIB: the tile (LDS) size, 8 (default) or 16 (tuning).  8
+// KiB tiles leave room for 8 resident workgroups per CU; 16 KiB (6 per CU,
+// LDS-bound) and 4 KiB (too little work per tile) ran slower
+// (profiles/r06/pack_tile_sizes.txt: struct {int; hole; double} 80.2 / 85.1 /
+// 92.9 us for 8 / 16 / 4 KiB against 91.4 for the unit kernel).
+static int pack_tile_bytes()
+{
+    static int b = 0;
+    if (!b) {
+        const char *e = getenv("MVX_PACK_TILE_KIB");
+        b = e && atoi(e) == 16 ? 16384 : PACK_TILE;
+    }
+    return b;
+}
+
+// elements per tile (a multiple of 16 / gcd(size, 16), its hull within
+// the tile with the alignment slack), or 0: the type does not tile
+static long pack_ept(const Type &t, long lo, long hi)
+{
+    const long TILE = pack_tile_bytes();
+    if (t.extent <= 0 || t.size <= 0 || hi - lo > TILE / 4) return 0;
+    long g = t.size, m = 16;
+    while (m) { const long r = g % m; g = m; m = r; }
+    const long step = 16 / g;
+    // hull of e elements: (e - 1) * ext + (hi - lo), plus up to 30 bytes of
+    // word alignment; spans reaching below the element (lo < 0) included
+    long e = (TILE - 32 - (hi - lo)) / t.extent + 1;
+    e -= e % step;
+    return e >= step ? e : 0;
+}
+
+template <int W>
+static int launch_tiles(Type &t, int wi, const void *src, void *dst, long count, long lo, long hi, long ept,
+                        hipStream_t st)
+{
+    const long tiles = (count + ept - 1) / ept;
+    if (tiles < 1 || tiles > INT32_MAX) return MPI_ERR_OTHER;
+    if (pack_tile_bytes() == 16384)
+        hipLaunchKernelGGL((k_pack_tiles<W, 16384>), dim3((unsigned)tiles), dim3(256), 0, st, (const char *)src,
+                           (char *)dst, (const int *)t.dunits[wi], t.units[wi], count, t.extent, lo, hi, ept);
+    else
+        hipLaunchKernelGGL((k_pack_tiles<W, PACK_TILE>), dim3((unsigned)tiles), dim3(256), 0, st, (const char *)src,
+                           (char *)dst, (const int *)t.dunits[wi], t.units[wi], count, t.extent, lo, hi, ept);
     return hipGetLastError() == hipSuccess ? MPI_SUCCESS : MPI_ERR_OTHER;
 }
 
@@ -842,6 +971,17 @@ static int pack(int h, const void *src, void *dst, size_t count, hipStream_t st,
         for (int wi = 0; units_on && wi < 3; ++wi) {
             const int W = Ws[wi];
             if (al % W || !unit_table(*t, W, wi)) continue;
+            if (packing && W < 16 && tiles_on() && (uintptr_t)dst % 16 == 0) {
+                long lo, hi;
+                if (!t->merge) t->merge = merge_ok(*t, &t->mlo, &t->mhi) ? 1 : -1;   // fills the reach too
+                lo = t->mlo;
+                hi = t->mhi;
+                const long ept = pack_ept(*t, lo, hi);
+                if (ept > 0) {
+                    if (W == 8) return launch_tiles<8>(*t, wi, src, dst, (long)count, lo, hi, ept, st);
+                    return launch_tiles<4>(*t, wi, src, dst, (long)count, lo, hi, ept, st);
+                }
+            }
             if (!packing && merge_on() && (uintptr_t)src % 16 == 0) {
                 if (!t->merge) t->merge = merge_ok(*t, &t->mlo, &t->mhi) ? 1 : -1;
                 if (t->merge > 0) {

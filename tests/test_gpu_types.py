@@ -311,7 +311,9 @@ def test_random_derived_sweep(mvx, oracle, types, batch):
 
 
 def test_whole_word_unpack_keeps_every_other_byte(mvx, oracle):
-    """Unpack of types whose maps leave holes inside 64-byte sectors runs by
+    """Pack through LDS tiles (k_pack_tiles, into a 16-byte-aligned packed
+    buffer) gives the unit kernel's stream (into a buffer 4 bytes off).
+    Unpack of types whose maps leave holes inside 64-byte sectors runs by
     whole 16-byte words (mvx_dtype.hip k_unpack_merge: each tile read into
     LDS, the units merged in, written back whole).  Against the oracle's
     type-map copy over a patterned buffer with guard bands: type-map bytes
@@ -346,6 +348,12 @@ def test_whole_word_unpack_keeps_every_other_byte(mvx, oracle):
                     dy = torch.from_numpy(y0).cuda()
                     dp = torch.zeros(max(n * size, 16), dtype=torch.uint8, device="cuda")
                     assert mvx.type_pack(h, dx.data_ptr() + off, dp, n) == 0
+                    # the same pack into a packed buffer 4 bytes off a 16-byte
+                    # boundary (no tiled pack there: the unit kernel) -- the
+                    # same stream
+                    dq = torch.zeros(max(n * size, 16) + 16, dtype=torch.uint8, device="cuda")
+                    assert mvx.type_pack(h, dx.data_ptr() + off, dq.data_ptr() + 4, n) == 0
+                    assert torch.equal(dq[4:4 + n * size], dp[:n * size]), (h, n, phase)
                     assert mvx.type_unpack(h, dp, dy.data_ptr() + off, n) == 0
                     ref = y0.copy()
                     assert oracle.type_copy(ref[off:], x[off:], n, h) == 0
