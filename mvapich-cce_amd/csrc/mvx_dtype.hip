@@ -819,8 +819,9 @@ static int launch_merge(Type &t, int wi, const void *src, void *dst, long count,
 // word holding one hull byte lies in the same page, so the read is safe),
 // then each lane gathers G = 16 / W units from LDS into one 16-byte chunk of
 // the packed stream and stores it whole.  A run's packed bytes start on a
-// 16-byte boundary (its element count is a multiple of 16 / gcd(size, 16));
-// the stream's last, partial chunk is stored unit by unit.
+// 64-byte boundary (its element count is a multiple of 64 / gcd(size, 64));
+// the stream's last, partial chunk is stored unit by unit.  (The kernel
+// needs only 16-byte tile starts; pack_ept makes them 64-byte ones.)
 #define PACK_TILE 8192               // LDS bytes of extent layout per workgroup
 
 template <int W, int TILE>
@@ -896,15 +897,16 @@ static int pack_tile_bytes()
     return b;
 }
 
-// elements per tile (a multiple of 16 / gcd(size, 16), its hull within
-// the tile with the alignment slack), or 0: the type does not tile
+// elements per tile (a multiple of 64 / gcd(size, 64): each tile's packed
+// bytes start on a 64-byte sector, so no two workgroups write one sector;
+// its hull within the tile with the alignment slack), or 0: no tiling
 static long pack_ept(const Type &t, long lo, long hi)
 {
     const long TILE = pack_tile_bytes();
     if (t.extent <= 0 || t.size <= 0 || hi - lo > TILE / 4) return 0;
-    long g = t.size, m = 16;
+    long g = t.size, m = 64;
     while (m) { const long r = g % m; g = m; m = r; }
-    const long step = 16 / g;
+    const long step = 64 / g;
     // hull of e elements: (e - 1) * ext + (hi - lo), plus up to 30 bytes of
     // word alignment; spans reaching below the element (lo < 0) included
     long e = (TILE - 32 - (hi - lo)) / t.extent + 1;

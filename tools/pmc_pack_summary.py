@@ -3,7 +3,7 @@
 rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE) over tools/bench_pack.py.
 
 bench_pack.py launches, per case in its order, 12 pack then 12 unpack
-dispatches; the pack-engine kernels (k_pack_units, k_pack, k_unpack_merge)
+dispatches; the pack-engine kernels (k_pack_units, k_pack, k_pack_tiles, k_unpack_merge)
 are taken in dispatch order and cut into groups of 12.  FETCH_SIZE is
 doubled (gfx950 tallies 128-byte requests at 64 B, MI355X_MICROARCH.md; exact
 for 16-B/lane streams); the counters are KiB, printed as MB (1e6 B).
@@ -17,7 +17,7 @@ import os
 import statistics
 import sys
 
-KERNELS = ("k_pack_units", "k_pack<", "k_unpack_merge")
+KERNELS = ("k_pack_units", "k_pack<", "k_unpack_merge", "k_pack_tiles")
 
 
 def rows(d, counter):
