@@ -32,6 +32,8 @@ Scenarios:
                             ranks device buffers
                reduce_dd    device buffers everywhere (non-roots pass a host
                             recvbuf, which the call never touches)
+               scan_dh      device sendbufs, host recvbufs on every rank
+                            but the last
   latency    an 8-byte device Allreduce (two floats) 300 times with the route
              agreed and 300 times under MVX_SHIM_ROUTE=local (no agreement),
              interleaved in blocks; reports each mode's median call time
@@ -171,7 +173,8 @@ def main():
             # (name, coll, send on device, recv on device) for this rank
             cases = [("reduce_dh", COLL_REDUCE, True, False), ("allreduce_dh", COLL_ALLREDUCE, True, False),
                      ("rs_hd", COLL_REDUCE_SCATTER, rank != 0, True),
-                     ("reduce_dd", COLL_REDUCE, True, rank == root)]
+                     ("reduce_dd", COLL_REDUCE, True, rank == root),
+                     ("scan_dh", COLL_SCAN, True, rank != root)]
             for name, coll, sd, rd in cases:
                 nrecv = cnts[rank] if coll == COLL_REDUCE_SCATTER else size
                 s = mk(S[rank], sd)
@@ -182,6 +185,8 @@ def main():
                     rc = call(tag, lambda: lib.h_allreduce(ptr(s), ptr(r), size, fnode, MPI_SUM))
                 elif coll == COLL_REDUCE:
                     rc = call(tag, lambda: lib.h_reduce(ptr(s), ptr(r), size, fnode, MPI_SUM, root))
+                elif coll == COLL_SCAN:
+                    rc = call(tag, lambda: lib.h_scan(ptr(s), ptr(r), size, fnode, MPI_SUM))
                 else:
                     rc = call(tag, lambda: lib.h_reduce_scatter(ptr(s), ptr(r), cn, fnode, MPI_SUM))
                 torch.cuda.synchronize()
@@ -193,6 +198,8 @@ def main():
                     O.allreduce(bs, be, size, FLOAT, MPI_SUM)
                 elif coll == COLL_REDUCE:
                     O.reduce(bs, be, size, FLOAT, MPI_SUM, root)
+                elif coll == COLL_SCAN:
+                    O.scan(bs, be, size, FLOAT, MPI_SUM)
                 else:
                     O.reduce_scatter(bs, be, cnts, FLOAT, MPI_SUM)
                 if coll == COLL_REDUCE and rank != root:

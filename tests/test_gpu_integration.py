@@ -174,13 +174,14 @@ def test_within_rank_kinds_through_the_shim(mvx, np_):
       Allreduce with device send and host recv on every rank;
       Reduce_scatter with host send and device recv on rank 0 only;
       Reduce with device buffers everywhere (the non-roots' host recvbuf is
-      never touched: the call is agreed all-device).
+      never touched: the call is agreed all-device);
+      Scan with device sendbufs and host recvbufs on all ranks but the last.
     Every rank's recvbuf is the oracle's replay bit for bit, at 1000 and
     300001 floats (the larger one in slices: MVX_SLICE_MIN_MIB=1)."""
     env = {"MVX_SLICE_MIN_MIB": "1", "MVX_SLICE_MIB": "1"}
     for rep in _world(np_, "kinds", {r: env for r in range(np_)}, timeout=300):
         assert not rep["fails"], rep
-        assert len(rep["calls"]) == 8
+        assert len(rep["calls"]) == 10
         for c in rep["calls"]:
             assert c["rc"] == 0 and c["host"] == 0 and c["agree"] in (1, 3), c
         dd = [c for c in rep["calls"] if c["name"].startswith("reduce_dd")]
