@@ -71,7 +71,10 @@ MVXI int mvxi_setmsg_code(int cls, int kind);
  * equal-size shards put the same chunk of every leaf at the same DRAM
  * interleave position, and the k-leaf combine then ran 5-6 % slower
  * (tools/tune_combine_layout.py, profiles/r01/tune_combine_layout.jsonl:
- * 53.9 vs 51.2 us for 8 x 32 MiB). */
+ * 53.9 vs 51.2 us for 8 x 32 MiB).  Re-swept in round 6 with the body
+ * kernel: 4 KiB still among the best (47.8-48.7 us; 0 / 512 B 51.6-52.6,
+ * 1.5-3 KiB 48.9-50.0, 3.5-12 KiB within 48.3-49.2:
+ * profiles/r06/tune_combine_layout_fine.jsonl). */
 #define SLOT_STAGGER 4096
 
 static inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }

@@ -57,8 +57,10 @@ def main():
         return e0.elapsed_time(e1) * 1e3 / reps
 
     alg = (k + 1) * leaf
-    sweep = "sweep" in sys.argv[1:]
-    kinds = ["slots", 256, 1024, 2048, 4096, 6144, 8192, 12288, 16384, 32768, "slots", 4096] if sweep else \
+    sweep = "sweep" in sys.argv[1:] or "fine" in sys.argv[1:]
+    kinds = [4096, 0, 512, 1536, 2560, 3072, 3584, 4096, 4352, 4608, 5120, 6144, 10240, 12288, 4096] \
+        if "fine" in sys.argv[1:] else \
+        ["slots", 256, 1024, 2048, 4096, 6144, 8192, 12288, 16384, 32768, "slots", 4096] if sweep else \
         ["separate", "slots", "stagger4k", "stagger64k", "stagger1m"]
     for kind in kinds:
         bufs = layout(kind)
