@@ -50,11 +50,12 @@ struct Type {
     // the map on the device, split into pieces of <= 64 bytes
     void *dmap;
     long dmap_n;
-    // the map as W-byte units (W = 16, 8, 4: index 0, 1, 2): each unit's
-    // offset in the element, in packed order; 0: not built; -1: the map
-    // does not split into W-byte units
-    int *dunits[3];
-    long units[3];
+    // the map as W-byte units (W = 16, 8, 4, 2, 1: index 0 .. 4): each
+    // unit's offset in the element, in packed order; 0: not built; -1: the
+    // map does not split into W-byte units (2 and 1 serve the tile kernels
+    // only)
+    int *dunits[5];
+    long units[5];
     // whole-word unpack (merge_ok): 0 not decided, 1 yes, -1 no; the map's
     // reach [mlo, mhi) around the element origin
     int merge;
@@ -74,7 +75,7 @@ static Type *slot(int h)
 static void reset(Type &t)
 {
     if (t.dmap) (void)hipFree(t.dmap);
-    for (int w = 0; w < 3; ++w)
+    for (int w = 0; w < 5; ++w)
         if (t.dunits[w]) (void)hipFree(t.dunits[w]);
     t = Type();
 }
@@ -551,6 +552,8 @@ k_pack(const char *__restrict__ src, char *__restrict__ dst, const DBlk *__restr
 typedef uint32_t pu32x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t pu32x4 __attribute__((ext_vector_type(4)));
 template <int W> struct UnitT;
+template <> struct UnitT<1> { typedef uint8_t t; };
+template <> struct UnitT<2> { typedef uint16_t t; };
 template <> struct UnitT<4> { typedef uint32_t t; };
 template <> struct UnitT<8> { typedef pu32x2 t; };
 template <> struct UnitT<16> { typedef pu32x4 t; };
@@ -671,6 +674,33 @@ template <> __device__ inline pu32x2 unit_of<8>(const pu32x4 &v, int g)
     return r;
 }
 template <> __device__ inline pu32x4 unit_of<16>(const pu32x4 &v, int) { return v; }
+template <> __device__ inline uint16_t unit_of<2>(const pu32x4 &v, int g)
+{
+    return (uint16_t)(v[g >> 1] >> (16 * (g & 1)));
+}
+template <> __device__ inline uint8_t unit_of<1>(const pu32x4 &v, int g)
+{
+    return (uint8_t)(v[g >> 2] >> (8 * (g & 3)));
+}
+
+// unit g (W bytes) of a 16-byte chunk being assembled
+template <int W> __device__ inline void set_unit(pu32x4 &v, int g, typename UnitT<W>::t x);
+template <> __device__ inline void set_unit<8>(pu32x4 &v, int g, pu32x2 x)
+{
+    v[2 * g] = x.x;
+    v[2 * g + 1] = x.y;
+}
+template <> __device__ inline void set_unit<4>(pu32x4 &v, int g, uint32_t x) { v[g] = x; }
+template <> __device__ inline void set_unit<2>(pu32x4 &v, int g, uint16_t x)
+{
+    const int s = 16 * (g & 1);
+    v[g >> 1] = (v[g >> 1] & ~(0xffffu << s)) | ((uint32_t)x << s);
+}
+template <> __device__ inline void set_unit<1>(pu32x4 &v, int g, uint8_t x)
+{
+    const int s = 8 * (g & 3);
+    v[g >> 2] = (v[g >> 2] & ~(0xffu << s)) | ((uint32_t)x << s);
+}
 
 template <int W, int TILE>
 __global__ void __launch_bounds__(256)
@@ -697,9 +727,16 @@ k_unpack_merge(const char *__restrict__ packed, char *__restrict__ dst, const in
     if (ihi > n) ihi = n;
     // the units of those elements, read 16 bytes of the packed stream (G
     // units) per lane, two chunks in flight; a chunk that runs past the
-    // stream's end is read unit by unit
+    // stream's end is read unit by unit.  Offsets from here are 32-bit and
+    // relative to the tile (an element's reach and the extent are bounded,
+    // merge_ok): unit j of element ilo + ir lands at ir * ext + e0 + uoff[j]
     constexpr int G = 16 / W;
-    const long qn = n * upe, c0 = ilo * upe / G, c1 = (ihi * upe + G - 1) / G;
+    const int up = (int)upe, ext32 = (int)ext, span = (int)(tend - t0);
+    const int e0 = (int)(ilo * ext - a);
+    const long q0 = ilo * upe, qn = n * upe, c0 = q0 / G, c1 = (ihi * upe + G - 1) / G;
+    // the words of the tile wholly inside the hull [h0, h1), tile-relative
+    const long hl = (long)(h0 - t0), hh = (long)(h1 - t0);
+    const int in_lo = hl < 0 ? 0 : (int)hl, in_hi = hh > span ? span : (int)hh;
     for (long c = c0 + threadIdx.x; c < c1; c += 512) {
         pu32x4 v[2];
 #pragma unroll
@@ -712,19 +749,21 @@ k_unpack_merge(const char *__restrict__ packed, char *__restrict__ dst, const in
             const long cc = c + 256 * u;
             if (cc >= c1) continue;
             const bool whole = (cc + 1) * G <= qn;
-            long q = cc * G, i = q / upe, j = q - i * upe;
+            long q = cc * G;
+            const int qr = (int)(q - q0);          // > -G: the first chunk may start in element ilo - 1
+            int ir = qr >= 0 ? qr / up : -1, j = qr >= 0 ? qr - ir * up : up + qr;
 #pragma unroll
             for (int g = 0; g < G; ++g, ++q) {
-                if (q < qn) {
-                    const long off = i * ext + (lds_units ? s_uoff[j] : uoff[j]);
-                    if (off >= a && off < b) {
+                if (q < qn && ir >= 0) {
+                    const int rel = ir * ext32 + e0 + (lds_units ? s_uoff[j] : uoff[j]);
+                    if ((unsigned)rel < (unsigned)span) {
                         const V x = whole ? unit_of<W>(v[u], g) : *(const V *)(packed + q * W);
-                        const uintptr_t at = (uintptr_t)dst + off, word = at & ~(uintptr_t)15;
-                        if (word < h0 || word + 16 > h1) *(V *)at = x;        // a word past the hull: its units only
-                        else *(V *)((char *)s_tile + (at - t0)) = x;
+                        const int word = rel & ~15;
+                        if (word < in_lo || word + 16 > in_hi) *(V *)(t0 + (uintptr_t)rel) = x;   // past the hull: units only
+                        else *(V *)((char *)s_tile + rel) = x;
                     }
                 }
-                if (++j == upe) { j = 0; ++i; }
+                if (++j == up) { j = 0; ++ir; }
             }
         }
     }
@@ -755,7 +794,7 @@ static int merge_on()
 // read and write).
 static bool merge_ok(const Type &t, long *lo, long *hi)
 {
-    if (t.map.empty() || t.extent <= 0) return false;
+    if (t.map.empty() || t.extent <= 0 || t.extent > (1L << 30)) return false;   // 32-bit tile offsets
     long l = t.map[0].off, h = t.map[0].off + t.map[0].len;
     for (const Blk &b : t.map) {
         if (b.off < l) l = b.off;
@@ -846,25 +885,27 @@ k_pack_tiles(const char *__restrict__ src, char *__restrict__ dst, const int *__
     __syncthreads();
     const long qn = n * upe, qlo = i0 * upe, qhi = i1 * upe;
     const long c0 = qlo / G, c1 = (qhi + G - 1) / G;      // qlo is a multiple of G (ept)
-    const long base = (long)(a0 - (uintptr_t)src);          // the tile's offset from src
+    // 32-bit, tile-relative from here (pack_ept bounds the extent): unit j
+    // of element i0 + ir sits at ir * ext + e0 + uoff[j] in the tile
+    const int up = (int)upe, ext32 = (int)ext;
+    const int e0 = (int)(i0 * ext - (long)(a0 - (uintptr_t)src));
     for (long c = c0 + threadIdx.x; c < c1; c += 256) {
-        long q = c * G, i = q / upe, j = q - i * upe;
+        const int qr = (int)(c * G - qlo);
+        int ir = qr / up, j = qr - ir * up;
         if ((c + 1) * G <= qn) {
-            pu32x4 out;
+            pu32x4 out = {0, 0, 0, 0};
 #pragma unroll
             for (int g = 0; g < G; ++g) {
-                const long off = i * ext + (lds_units ? s_uoff[j] : uoff[j]) - base;
-                const V x = *(const V *)((const char *)s_tile + off);
-                if constexpr (W == 4) out[g] = x;
-                else { out[2 * g] = x.x; out[2 * g + 1] = x.y; }
-                if (++j == upe) { j = 0; ++i; }
+                const int rel = ir * ext32 + e0 + (lds_units ? s_uoff[j] : uoff[j]);
+                set_unit<W>(out, g, *(const V *)((const char *)s_tile + rel));
+                if (++j == up) { j = 0; ++ir; }
             }
             __builtin_nontemporal_store(out, (pu32x4 *)(dst + 16 * c));
         } else {
-            for (int g = 0; g < G && q < qn; ++g, ++q) {
-                const long off = i * ext + (lds_units ? s_uoff[j] : uoff[j]) - base;
-                *(V *)(dst + q * W) = *(const V *)((const char *)s_tile + off);
-                if (++j == upe) { j = 0; ++i; }
+            for (long q = c * G; q < qn; ++q) {
+                const int rel = ir * ext32 + e0 + (lds_units ? s_uoff[j] : uoff[j]);
+                *(V *)(dst + q * W) = *(const V *)((const char *)s_tile + rel);
+                if (++j == up) { j = 0; ++ir; }
             }
         }
     }
@@ -903,7 +944,7 @@ static int pack_tile_bytes()
 static long pack_ept(const Type &t, long lo, long hi)
 {
     const long TILE = pack_tile_bytes();
-    if (t.extent <= 0 || t.size <= 0 || hi - lo > TILE / 4) return 0;
+    if (t.extent <= 0 || t.extent > (1L << 30) || t.size <= 0 || hi - lo > TILE / 4) return 0;
     long g = t.size, m = 64;
     while (m) { const long r = g % m; g = m; m = r; }
     const long step = 64 / g;
@@ -998,6 +1039,31 @@ static int pack(int h, const void *src, void *dst, size_t count, hipStream_t st,
                                        : launch_units<false, 8>(*t, wi, src, dst, (long)count, st);
             return packing ? launch_units<true, 4>(*t, wi, src, dst, (long)count, st)
                            : launch_units<false, 4>(*t, wi, src, dst, (long)count, st);
+        }
+    }
+    {
+        // maps with 2- or 1-byte pieces: the tile kernels over 2- or 1-byte
+        // units where they apply, else the piece kernel below
+        static int units_on = -1;
+        if (units_on < 0) {
+            const char *e = getenv("MVX_PACK_UNITS");
+            units_on = e ? atoi(e) != 0 : 1;
+        }
+        const uintptr_t al = (uintptr_t)src | (uintptr_t)dst;
+        for (int wi = 3; units_on && t->size <= 4096 && wi < 5; ++wi) {   // small elements only
+            const int W = wi == 3 ? 2 : 1;
+            if (al % W || !unit_table(*t, W, wi)) continue;
+            if (!t->merge) t->merge = merge_ok(*t, &t->mlo, &t->mhi) ? 1 : -1;
+            if (packing && tiles_on() && (uintptr_t)dst % 16 == 0) {
+                const long ept = pack_ept(*t, t->mlo, t->mhi);
+                if (ept > 0)
+                    return W == 2 ? launch_tiles<2>(*t, wi, src, dst, (long)count, t->mlo, t->mhi, ept, st)
+                                  : launch_tiles<1>(*t, wi, src, dst, (long)count, t->mlo, t->mhi, ept, st);
+            }
+            if (!packing && merge_on() && (uintptr_t)src % 16 == 0 && t->merge > 0)
+                return W == 2 ? launch_merge<2>(*t, wi, src, dst, (long)count, t->mlo, t->mhi, st)
+                              : launch_merge<1>(*t, wi, src, dst, (long)count, t->mlo, t->mhi, st);
+            break;
         }
     }
     int rc = device_map(*t);

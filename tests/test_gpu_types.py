@@ -320,7 +320,9 @@ def test_whole_word_unpack_keeps_every_other_byte(mvx, oracle):
     land, holes and guards keep their pattern -- at counts 1, 2, 3, 1000
     and 100003, with the origin at every 4-byte phase of a 16-byte word (the
     first and last words of the hull are partial there and take unit stores
-    instead), and for a type reaching below its origin (negative stride)."""
+    instead), for a type reaching below its origin (negative stride), and
+    for maps of 1- and 2-byte pieces (the tile kernels over 1- and 2-byte
+    units)."""
     import torch
     made = [
         _both(mvx, oracle, "vector", 8, 1, 4, D),              # 8 B of every 32
@@ -328,6 +330,10 @@ def test_whole_word_unpack_keeps_every_other_byte(mvx, oracle):
         _both(mvx, oracle, "struct", 2, [1, 1], [0, 8], [I, D]),  # {int; hole; double}
         _both(mvx, oracle, "hvector", 3, 1, -20, I),           # reaches below the origin
         _both(mvx, oracle, "hindexed", 3, [1, 2, 1], [0, 12, 40], F),
+        _both(mvx, oracle, "vector", 2, 1, 2, C),              # every other byte (1-byte units)
+        _both(mvx, oracle, "struct", 2, [1, 1], [0, 4], [C, I]),  # {char; hole; int}
+        _both(mvx, oracle, "hvector", 3, 1, 6, 4),             # shorts 6 bytes apart (2-byte units)
+        _both(mvx, oracle, "hindexed", 3, [3, 1, 2], [1, 9, 13], C),   # bytes from 1, odd spans
     ]
     try:
         for h in made:

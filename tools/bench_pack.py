@@ -52,6 +52,10 @@ def main():
         ("vector(4,1000,1024,FLOAT) 4000 B of every 4096", mvx.MPI_Type_vector, (4, 1000, 1024, F),
          vec(4, 1000, 1024, 4)),
         ("struct{int; hole; double} 12 B of 16", mvx.MPI_Type_struct, (2, [1, 1], [0, 8], [I, D]), [(0, 4), (8, 8)]),
+        ("vector(2,1,2,CHAR) every other byte", mvx.MPI_Type_vector, (2, 1, 2, mvx.MPI_CHAR), vec(2, 1, 2, 1)),
+        ("struct{char; hole; int} 5 B of 8", mvx.MPI_Type_struct, (2, [1, 1], [0, 4], [mvx.MPI_CHAR, I]),
+         [(0, 1), (4, 4)]),
+        ("vector(4,1,2,SHORT) every other short", mvx.MPI_Type_vector, (4, 1, 2, mvx.MPI_SHORT), vec(4, 1, 2, 2)),
     ]
     stream = torch.cuda.current_stream()
     for name, ctor, args, blocks in cases:

@@ -1,0 +1,13 @@
+# Round-6 session p: HBM bytes of the final pack / unpack kernels (PMC, one
+# counter per pass) over tools/bench_pack.py.
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 300 python3 tools/bench_pack.py > gpurun_out/r06p_pack_on.jsonl 2> gpurun_out/r06p_pack_on.err || { tail -20 gpurun_out/r06p_pack_on.err; exit 1; }
+for c in FETCH_SIZE WRITE_SIZE; do
+  rm -rf gpurun_out/r06p_pmc_$c
+  timeout -s KILL 240 rocprofv3 --pmc $c --output-format csv -d gpurun_out/r06p_pmc_$c -o p -- python3 tools/bench_pack.py \
+    > gpurun_out/r06p_pmc_$c.log 2>&1 || { tail -20 gpurun_out/r06p_pmc_$c.log; exit 1; }
+done
+python3 tools/pmc_pack_summary.py gpurun_out/r06p_pmc_FETCH_SIZE gpurun_out/r06p_pmc_WRITE_SIZE gpurun_out/r06p_pack_on.jsonl > gpurun_out/r06p_pmc_pack.txt || exit 1
+cut -c1-175 gpurun_out/r06p_pmc_pack.txt
