@@ -104,9 +104,10 @@ int mvx_host_register_stats(long *entries, size_t *bytes, long *hits, long *miss
 /* registrations dropped by releases (hooks and mvx_host_invalidate) so far */
 long mvx_host_register_invalidations(void);
 /* dropped registrations not unregistered yet, registrations held by calls in
- * flight, and hipHostUnregister calls made so far (in dry mode: that would
- * have been made) */
-int mvx_host_register_deferred(long *deferred, long *held, long *unregisters);
+ * flight, hipHostUnregister calls made so far (in dry mode: that would have
+ * been made), and ranges copied through the CPU because their pages were
+ * partly under a registration in use by another call */
+int mvx_host_register_deferred(long *deferred, long *held, long *unregisters, long *bounced);
 
 /* The buffer kinds of every rank in the next blocking collective call on
  * `comm`, when the caller has agreed them across ranks (the MVAPICH shim

@@ -148,7 +148,7 @@ def _load():
     c.mvx_host_register_invalidations.restype = ctypes.c_long
     c.mvx_host_register_stats.argtypes = [ctypes.POINTER(ctypes.c_long), ctypes.POINTER(ctypes.c_size_t),
                                           ctypes.POINTER(ctypes.c_long), ctypes.POINTER(ctypes.c_long)]
-    c.mvx_host_register_deferred.argtypes = [ctypes.POINTER(ctypes.c_long)] * 3
+    c.mvx_host_register_deferred.argtypes = [ctypes.POINTER(ctypes.c_long)] * 4
     c.mvx_copy.argtypes = [vp, vp, sz]
     c.mvx_stream_synchronize.argtypes = [vp]
     c.mvx_comm_free.argtypes = [pi]

@@ -536,10 +536,12 @@ def host_register_stats():
 
 
 def host_register_deferred():
-    """{deferred, held, unregisters}: registrations a release dropped that
-    are not unregistered yet (a call still holds them, or no libmvx entry
-    has run since), registrations held by calls in flight, and the
-    hipHostUnregister calls made so far (mvx_host_register_deferred)."""
-    d, h, u = ctypes.c_long(), ctypes.c_long(), ctypes.c_long()
-    coll().mvx_host_register_deferred(ctypes.byref(d), ctypes.byref(h), ctypes.byref(u))
-    return {"deferred": d.value, "held": h.value, "unregisters": u.value}
+    """{deferred, held, unregisters, bounced}: registrations a release
+    dropped that are not unregistered yet (a call still holds them, or no
+    libmvx entry has run since), registrations held by calls in flight, the
+    hipHostUnregister calls made so far, and ranges copied through the CPU
+    because another call's registration covered part of their pages
+    (mvx_host_register_deferred)."""
+    d, h, u, b = ctypes.c_long(), ctypes.c_long(), ctypes.c_long(), ctypes.c_long()
+    coll().mvx_host_register_deferred(ctypes.byref(d), ctypes.byref(h), ctypes.byref(u), ctypes.byref(b))
+    return {"deferred": d.value, "held": h.value, "unregisters": u.value, "bounced": b.value}

@@ -111,9 +111,7 @@ static int run_on(mvx_comm_t *c, const call_t *k, hipStream_t st, int blocking)
         /* MPIR_intra_Scan ignores MPIR_Op_errno: recvbuf keeps the self copy
          * (intra_scan.c:100-106) and the call succeeds */
         if (Pp->packed) return mvxi_typed_copy(c, k->dt, nsend, k->sendbuf, k->recvbuf, st, blocking);
-        if (hipMemcpyAsync(k->recvbuf, k->sendbuf, (size_t)(nsend * e), hipMemcpyDefault, st) != hipSuccess)
-            return MPI_ERR_OTHER;
-        return (blocking && hipStreamSynchronize(st) != hipSuccess) ? MPI_ERR_OTHER : MPI_SUCCESS;
+        return mvxi_copy_any(c, k->recvbuf, k->sendbuf, (size_t)(nsend * e), st, blocking);
     }
     if (verdict == MVX_ERR_OP_NOT_DEFINED) {
         /* 329 on the ranks that call (*uop); the data still moves as the
@@ -387,9 +385,8 @@ static int run_multi_on(mvx_comm_t *c, int coll, void *const *sendbufs,
             if (coll == MVX_COLL_SCAN && verdict == MVX_ERR_OP_NOT_DEFINED && count > 0) {
                 if (plans[r].packed) {
                     if ((rc = mvxi_typed_copy(c, dt, count, sendbufs[r], recvbufs[r], st, 1))) return rc;
-                } else if (hipMemcpyAsync(recvbufs[r], sendbufs[r], (size_t)(count * e), hipMemcpyDefault, st) !=
-                           hipSuccess) {
-                    return MPI_ERR_OTHER;
+                } else if ((rc = mvxi_copy_any(c, recvbufs[r], sendbufs[r], (size_t)(count * e), st, 0))) {
+                    return rc;
                 }
             }
         }
@@ -409,7 +406,8 @@ static int run_multi_on(mvx_comm_t *c, int coll, void *const *sendbufs,
         mvxi_xport_loopback(&t[r], &w->lb, r);
     }
     J->kinds = 0;
-    host = mvxi_job_kinds(J);
+    /* a packed job asks its spans' kinds itself (packed_setup) */
+    host = plans[0].packed ? mvxi_job_packed_host(J) : mvxi_job_kinds(J);
     c->keep = verdict == MVX_ERR_OP_NOT_DEFINED;    /* the transfers of an undefined pair */
     if (plans[0].packed) rc = mvxi_run_job_packed(c, J, st, host);
     else rc = host ? mvxi_run_staged(c, J, st) : mvxi_run_device(c, J, st);

@@ -212,19 +212,52 @@ int mvxi_recv_ranges(const mvx_plan *Q, mvx_range *v)
 /* the buffers' kinds, one pointer query each (pageable ranges may come back
  * pinned from the registration cache, held for the job until
  * mvxi_job_release); returns 1 if any is host memory */
+/* operand q of the job (2r: send of rank r, 2r + 1: its recv) */
+static void job_operand(job_t *J, int q, const char **p, size_t *bytes, int **kind, unsigned long **hold)
+{
+    const int r = q >> 1;
+    const size_t E = (size_t)J->P[r].esize;
+    if (q & 1) { *p = J->recv[r]; *bytes = (size_t)J->nrecv[r] * E; *kind = &J->rkind[r]; *hold = &J->rhold[r]; }
+    else { *p = J->send[r]; *bytes = (size_t)J->nsend[r] * E; *kind = &J->skind[r]; *hold = &J->shold[r]; }
+}
+
 int mvxi_job_kinds(job_t *J)
 {
     int r, host = 0;
     if (!J->kinds) {
-        for (r = 0; r < J->nr; r++) {
-            const size_t E = (size_t)J->P[r].esize;
-            J->shold[r] = J->rhold[r] = 0;
-            J->skind[r] = J->nsend[r] > 0
-                              ? mvxi_buf_kind_hold(J->send[r], (size_t)J->nsend[r] * E, &J->shold[r])
-                              : MVX_BUF_DEVICE;
-            J->rkind[r] = J->nrecv[r] > 0
-                              ? mvxi_buf_kind_hold(J->recv[r], (size_t)J->nrecv[r] * E, &J->rhold[r])
-                              : MVX_BUF_DEVICE;
+        unsigned long *mine[2 * MVX_MAXP];
+        int q, nmine = 0, pass;
+        for (q = 0; q < 2 * J->nr; q++) {
+            const char *p;
+            size_t bytes;
+            int *kind;
+            unsigned long *hold;
+            job_operand(J, q, &p, &bytes, &kind, &hold);
+            *hold = 0;
+            *kind = bytes ? mvxi_buf_kind_hold(p, bytes, hold, mine, nmine) : MVX_BUF_DEVICE;
+            if (*hold) mine[nmine++] = hold;
+        }
+        /* an operand whose registration was merged into another's union and
+         * then lost (the union could not be registered) is asked again */
+        for (pass = 0; pass < 2 * J->nr; pass++) {
+            int again = 0;
+            for (q = 0; q < 2 * J->nr; q++) {
+                const char *p;
+                size_t bytes;
+                int *kind, i, n = 0;
+                unsigned long *hold, *others[2 * MVX_MAXP];
+                job_operand(J, q, &p, &bytes, &kind, &hold);
+                if (*kind != MVX_BUF_PINNED || *hold || !bytes || mvx_host_pinned(p) == 1) continue;
+                for (i = 0; i < nmine; i++)
+                    if (mine[i] != hold) others[n++] = mine[i];
+                *kind = mvxi_buf_kind_hold(p, bytes, hold, others, n);
+                if (*hold) {
+                    for (i = 0; i < nmine && mine[i] != hold; i++) ;
+                    if (i == nmine) mine[nmine++] = hold;
+                }
+                again = 1;
+            }
+            if (!again) break;
         }
         J->kinds = 1;
     }

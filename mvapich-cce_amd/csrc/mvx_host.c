@@ -249,7 +249,7 @@ static struct {
     pthread_mutex_t mu;
     int init, on, dry;
     size_t min_bytes, max_bytes, total;
-    unsigned long clock, next_id, hits, misses, evictions, failures, invalidations;
+    unsigned long clock, next_id, hits, misses, evictions, failures, invalidations, bounced;
     int n, nd;
     reg_t e[REG_MAX];              /* the table: registered, findable */
     reg_t d[REG_DEFER];            /* deferred: released, still registered until unheld and flushed */
@@ -450,7 +450,7 @@ long mvx_host_register_invalidations(void)
     return n;
 }
 
-int mvx_host_register_deferred(long *deferred, long *held, long *unregisters)
+int mvx_host_register_deferred(long *deferred, long *held, long *unregisters, long *bounced)
 {
     int i;
     long h = 0;
@@ -459,29 +459,40 @@ int mvx_host_register_deferred(long *deferred, long *held, long *unregisters)
     for (i = 0; i < g_reg.nd; i++) h += g_reg.d[i].hold > 0;
     if (deferred) *deferred = g_reg.nd;
     if (held) *held = h;
+    if (bounced) *bounced = (long)g_reg.bounced;
     pthread_mutex_unlock(&g_reg.mu);
     if (unregisters) *unregisters = __atomic_load_n(&g_reg_unregisters, __ATOMIC_RELAXED);
     return 0;
 }
 
+/* how many of the caller's holds (mine[]) are on entry id */
+static int mine_on(unsigned long id, unsigned long *const *mine, int nmine)
+{
+    int i, n = 0;
+    for (i = 0; i < nmine; i++) n += *mine[i] == id;
+    return n;
+}
+
 /* Register [p, p + bytes) (page-widened) in the cache; MVX_BUF_PINNED when
- * the range is (now) registered, else what mvx_buf_kind says, or
- * MVX_BUF_PAGEABLE where the pages are under a registration the cache cannot
- * hand out (deferred, held by a merge candidate, in progress elsewhere) --
- * the bounce path then copies with the CPU.  `k` is p's kind as mvx_buf_kind
- * reported it (after a flush).  With `id`, a call's hold is taken on the
- * entry and its id stored (0: none). */
-static int reg_range(const void *p, size_t bytes, int k, unsigned long *id)
+ * the range is (now) registered, MVX_BUF_BOUNCE when its pages are partly
+ * under a registration the cache cannot merge it with (held by another
+ * call, deferred, or being registered by another thread), else what
+ * mvx_buf_kind says.  `k` is p's kind as mvx_buf_kind reported it (after a
+ * flush).  With `id`, a call's hold is taken on the entry and its id stored
+ * (0: none); mine[0..nmine) are the call's earlier holds (mvxi_buf_kind_hold). */
+static int reg_range(const void *p, size_t bytes, int k, unsigned long *id, unsigned long *const *mine, int nmine)
 {
     const uintptr_t ulo = (uintptr_t)p, uhi = (uintptr_t)p + bytes;
     uintptr_t base, end;
     reg_out_t out;
-    int i, cover = -1, overlap = 0, dry, ok, f = -1, conflict;
+    int i, cover = -1, overlap = 0, dry, ok, f = -1, conflict, carried = 0;
+    unsigned long merged[REG_MAX];
+    int nmerged = 0;
     hipError_t hr = hipSuccess;
     if (id) *id = 0;
     pthread_mutex_lock(&g_reg.mu);
     reg_env();
-    if (!g_reg.on && !g_reg.n) { pthread_mutex_unlock(&g_reg.mu); return k; }
+    if (!g_reg.on && !g_reg.n && !g_reg.nd) { pthread_mutex_unlock(&g_reg.mu); return k; }
     base = ulo & ~(PAGE - 1);
     end = (uhi + PAGE - 1) & ~(PAGE - 1);
     for (i = 0; i < g_reg.n; i++) {
@@ -499,23 +510,31 @@ static int reg_range(const void *p, size_t bytes, int k, unsigned long *id)
         return MVX_BUF_PINNED;
     }
     for (i = 0; i < g_reg.nd; i++)                       /* released pages still pinned for a call */
-        if (overlaps(g_reg.d[i].base, g_reg.d[i].end, base, end)) { pthread_mutex_unlock(&g_reg.mu); return MVX_BUF_PAGEABLE; }
+        if (overlaps(g_reg.d[i].base, g_reg.d[i].end, base, end)) {
+            g_reg.bounced++;
+            pthread_mutex_unlock(&g_reg.mu);
+            return MVX_BUF_BOUNCE;
+        }
     for (i = 0; i < REG_FLY; i++)
         if (g_reg.fly[i].used && overlaps(g_reg.fly[i].base, g_reg.fly[i].end, base, end)) {
+            g_reg.bounced++;
             pthread_mutex_unlock(&g_reg.mu);
-            return MVX_BUF_PAGEABLE;
+            return MVX_BUF_BOUNCE;
         }
     if (k == MVX_BUF_PINNED && !overlap) {              /* the caller's own page-locked memory */
         pthread_mutex_unlock(&g_reg.mu);
         return k;
     }
     /* a range that runs past a registration of ours: the union replaces it
-     * (a DMA must never read past the pinned pages) -- unless a call is
-     * using that registration */
+     * (a DMA must never read past the pinned pages) -- unless another call
+     * is using that registration.  This call's own holds (its other
+     * operands, no DMA issued yet) move to the union. */
     for (i = 0; i < g_reg.n; i++)
-        if (g_reg.e[i].hold && overlaps(g_reg.e[i].base, g_reg.e[i].end, base, end)) {
+        if (g_reg.e[i].hold && overlaps(g_reg.e[i].base, g_reg.e[i].end, base, end) &&
+            g_reg.e[i].hold != mine_on(g_reg.e[i].id, mine, nmine)) {
+            g_reg.bounced++;
             pthread_mutex_unlock(&g_reg.mu);
-            return MVX_BUF_PAGEABLE;
+            return MVX_BUF_BOUNCE;
         }
     out.n = 0;
     {
@@ -526,6 +545,7 @@ static int reg_range(const void *p, size_t bytes, int k, unsigned long *id)
                 if (g_reg.e[i].end > end) end = g_reg.e[i].end;
                 if (g_reg.e[i].ulo < u0) u0 = g_reg.e[i].ulo;
                 if (g_reg.e[i].uhi > u1) u1 = g_reg.e[i].uhi;
+                if (g_reg.e[i].hold) { merged[nmerged++] = g_reg.e[i].id; carried += g_reg.e[i].hold; }
                 reg_take_locked(i, &out);
             }
         ok = g_reg.on && end - base >= g_reg.min_bytes && end - base <= g_reg.max_bytes && g_reg.nd < REG_MAX;
@@ -547,11 +567,25 @@ static int reg_range(const void *p, size_t bytes, int k, unsigned long *id)
             g_reg.fly[f].used = 1; g_reg.fly[f].stale = 0;
         }
     }
+    /* this call's holds on the registrations just taken out: dropped here
+     * (their ranges are unregistered below); if the union is registered
+     * they move to it, else those operands read as unregistered -- the
+     * caller re-reads their kinds (mvxi_buf_kind_hold returns the union's
+     * verdict for them through `mine`) */
+    for (i = 0; i < nmine; i++) {
+        int m;
+        for (m = 0; m < nmerged; m++)
+            if (*mine[i] == merged[m]) *mine[i] = ~0UL;   /* moved: resolved below */
+    }
     reg_span_locked();
     dry = g_reg.dry;
     pthread_mutex_unlock(&g_reg.mu);
     reg_release(&out, dry);
-    if (!ok) return mvx_buf_kind(p);
+    if (!ok) {
+        for (i = 0; i < nmine; i++)
+            if (*mine[i] == ~0UL) *mine[i] = 0;           /* the operand lost its registration */
+        return mvx_buf_kind(p);
+    }
     if (!dry) {                                          /* dreg_register */
         t_in_reg++;
         hr = hipHostRegister((void *)base, end - base, hipHostRegisterDefault);
@@ -574,32 +608,41 @@ static int reg_range(const void *p, size_t bytes, int k, unsigned long *id)
             e->base = base; e->end = end; e->ulo = fl->ulo; e->uhi = fl->uhi;
             e->stamp = ++g_reg.clock;
             e->id = ++g_reg.next_id;
-            e->hold = id ? 1 : 0;
+            e->hold = (id ? 1 : 0) + carried;
             if (id) *id = e->id;
+            for (i = 0; i < nmine; i++)
+                if (*mine[i] == ~0UL) *mine[i] = e->id;   /* the operands merged in hold the union */
             g_reg.total += end - base;
         }
     }
     reg_span_locked();
     pthread_mutex_unlock(&g_reg.mu);
+    if (hr != hipSuccess || conflict) {
+        for (i = 0; i < nmine; i++)
+            if (*mine[i] == ~0UL) *mine[i] = 0;
+    }
     if (hr != hipSuccess) return mvx_buf_kind(p);
     if (conflict) {
         reg_unregister(base, dry);
-        return MVX_BUF_PAGEABLE;
+        pthread_mutex_lock(&g_reg.mu);
+        g_reg.bounced++;
+        pthread_mutex_unlock(&g_reg.mu);
+        return MVX_BUF_BOUNCE;
     }
     return MVX_BUF_PINNED;
 }
 
-int mvxi_buf_kind_hold(const void *p, size_t bytes, unsigned long *hold)
+int mvxi_buf_kind_hold(const void *p, size_t bytes, unsigned long *hold, unsigned long *const *mine, int nmine)
 {
     const int k = mvx_buf_kind(p);                      /* flushes the deferred entries first */
     if (hold) *hold = 0;
     if (k == MVX_BUF_DEVICE || !p || !bytes) return k;
-    return reg_range(p, bytes, k, hold);
+    return reg_range(p, bytes, k, hold, mine, nmine);
 }
 
 int mvxi_buf_kind_range(const void *p, size_t bytes)
 {
-    return mvxi_buf_kind_hold(p, bytes, NULL);
+    return mvxi_buf_kind_hold(p, bytes, NULL, NULL, 0);
 }
 
 /* a call's last DMA on the entry is done */
@@ -627,7 +670,7 @@ int mvx_host_register(const void *addr, size_t bytes)
     on = g_reg.on;
     pthread_mutex_unlock(&g_reg.mu);
     if (!on) return MPI_ERR_OTHER;
-    return reg_range(addr, bytes, g_reg.dry ? MVX_BUF_PAGEABLE : mvx_buf_kind(addr), NULL) == MVX_BUF_PINNED
+    return reg_range(addr, bytes, g_reg.dry ? MVX_BUF_PAGEABLE : mvx_buf_kind(addr), NULL, NULL, 0) == MVX_BUF_PINNED
                ? MPI_SUCCESS : MPI_ERR_OTHER;
 }
 

@@ -98,8 +98,9 @@ static void *host_dev_alias(const void *p)
 }
 
 static int host_apply_locked(MPI_Op op, MPI_Datatype t, const char *in, char *inout, long len,
-                             int in_dev, int io_dev, int in_pin, int io_pin)
+                             int in_dev, int io_dev, int kin, int kio)
 {
+    const int in_pin = kin == MVX_BUF_PINNED, io_pin = kio == MVX_BUF_PINNED;
     int e, ts, rc, bounce_in, bounce_io;
     long chunk, c, nch, lag;
     size_t bytes, cb, slot;
@@ -115,8 +116,10 @@ static int host_apply_locked(MPI_Op op, MPI_Datatype t, const char *in, char *in
             return hipStreamSynchronize(g_hop.s[0]) == hipSuccess ? MPI_SUCCESS : MPI_ERR_OTHER;
         }
     }
-    bounce_in = !in_dev && bytes >= (size_t)HOP_BOUNCE_MIN && !in_pin;
-    bounce_io = !io_dev && bytes >= (size_t)HOP_BOUNCE_MIN && !io_pin;
+    /* pageable memory partly under another call's registration is never
+     * handed to HIP (MVX_BUF_BOUNCE): bounced at any size */
+    bounce_in = !in_dev && !in_pin && (bytes >= (size_t)HOP_BOUNCE_MIN || kin == MVX_BUF_BOUNCE);
+    bounce_io = !io_dev && !io_pin && (bytes >= (size_t)HOP_BOUNCE_MIN || kio == MVX_BUF_BOUNCE);
     /* chunk: whole 256-element groups (the device operands keep the kernel's
      * 16-byte vector path) */
     if (bounce_in || bounce_io) {       /* pool copies pace the pipeline: ~8 chunks */
@@ -204,9 +207,15 @@ static int host_apply(MPI_Op op, MPI_Datatype t, const char *in, char *inout, lo
     bytes = (size_t)len * e;
     pthread_mutex_lock(&g_hop_mu);
     {
-        const int in_pin = !in_dev && mvxi_buf_kind_hold(in, bytes, &hin) == MVX_BUF_PINNED;
-        const int io_pin = !io_dev && mvxi_buf_kind_hold(inout, bytes, &hio) == MVX_BUF_PINNED;
-        rc = host_apply_locked(op, t, in, inout, len, in_dev, io_dev, in_pin, io_pin);
+        unsigned long *mine[1] = {&hin};
+        int kin = in_dev ? MVX_BUF_DEVICE : mvxi_buf_kind_hold(in, bytes, &hin, NULL, 0);
+        const int kio = io_dev ? MVX_BUF_DEVICE : mvxi_buf_kind_hold(inout, bytes, &hio, mine, hin ? 1 : 0);
+        /* in's registration merged into inout's union and lost with it */
+        if (kin == MVX_BUF_PINNED && !hin && !mvx_host_pinned(in)) {
+            unsigned long *other[1] = {&hio};
+            kin = mvxi_buf_kind_hold(in, bytes, &hin, other, hio ? 1 : 0);
+        }
+        rc = host_apply_locked(op, t, in, inout, len, in_dev, io_dev, kin, kio);
     }
     if (rc != MPI_SUCCESS && (hin || hio)) {
         if (g_hop.s[0]) (void)hipStreamSynchronize(g_hop.s[0]);

@@ -40,6 +40,12 @@
 #define MVX_BUF_PAGEABLE 0   /* host memory the DMA engines cannot address */
 #define MVX_BUF_PINNED   1   /* page-locked host memory */
 #define MVX_BUF_DEVICE   2   /* device or managed memory */
+/* pageable memory whose pages a registration of the cache partly covers
+ * (a neighbour's, in use by another call): HIP refuses a copy that starts
+ * inside a registration and runs past it (hipErrorInvalidValue,
+ * tools/shadow_probe.c), so such memory is copied by the CPU through pinned
+ * bounce slots, never handed to HIP (mvx_host.c) */
+#define MVX_BUF_BOUNCE   3
 int mvx_buf_kind(const void *p);   /* one pointer-attribute query */
 int mvx_host_pinned(const void *p);
 int mvxi_host_drain_lag(void);
@@ -52,8 +58,12 @@ MVXI int mvxi_buf_kind_range(const void *p, size_t bytes);
 /* the same, for a call that will DMA the range: a range the cache hands out
  * as registered is held for the call (*hold its id, 0 if none) until
  * mvxi_buf_release(hold) after the call's last DMA on it -- a release of its
- * memory meanwhile defers the unregistration (mvx_host.c) */
-MVXI int mvxi_buf_kind_hold(const void *p, size_t bytes, unsigned long *hold);
+ * memory meanwhile defers the unregistration (mvx_host.c).  mine[0..nmine)
+ * point at the holds this call took already, before any of its DMA: a
+ * registration only this call holds may still be merged with the new range
+ * (its operands sharing a page), and the ids there are updated if it is. */
+MVXI int mvxi_buf_kind_hold(const void *p, size_t bytes, unsigned long *hold, unsigned long *const *mine,
+                            int nmine);
 MVXI void mvxi_buf_release(unsigned long hold);
 MVXI hipError_t mvxi_queue_stream(hipStream_t *s, const char *env, const char *dflt);
 
@@ -176,7 +186,9 @@ typedef struct {                  /* a communicator's host-staging resources */
 } stage_res_t;
 
 MVXI int mvxi_run_job(mvx_comm_t *c, job_t *J, hipStream_t st, int blocking);
-MVXI int mvxi_run_job_packed(mvx_comm_t *c, const job_t *J, hipStream_t st, int blocking);
+MVXI int mvxi_run_job_packed(mvx_comm_t *c, job_t *J, hipStream_t st, int blocking);
+MVXI int mvxi_job_packed_host(const job_t *J);
+MVXI int mvxi_copy_any(mvx_comm_t *c, void *dst, const void *src, size_t bytes, hipStream_t st, int sync);
 MVXI int mvxi_run_staged(mvx_comm_t *c, const job_t *J, hipStream_t st);
 MVXI int mvxi_typed_copy(mvx_comm_t *c, int dt, long n, const char *send, char *recv, hipStream_t st, int sync);
 MVXI void mvxi_stage_release(stage_res_t *S);

@@ -283,7 +283,7 @@ static int run_staged_cs(mvx_comm_t *c, const job_t *J, hipStream_t st, long cs_
 
 static int mirror_bounced(int kind, size_t bytes)
 {
-    return kind == MVX_BUF_PAGEABLE && bytes >= (size_t)MIRROR_BOUNCE_MIN;
+    return kind == MVX_BUF_BOUNCE || (kind == MVX_BUF_PAGEABLE && bytes >= (size_t)MIRROR_BOUNCE_MIN);
 }
 
 static int mirror_in(stage_res_t *R, char *dev, const char *host, size_t bytes, int kind, hipStream_t st)
@@ -403,39 +403,75 @@ static size_t span_bytes(const tspan_t *T, long n)
 }
 
 
-static int packed_setup(mvx_comm_t *c, const job_t *J, const tspan_t *T, packed_bufs_t *B, hipStream_t st)
+/* the kinds of the host spans a packed job copies (the type maps' hull of
+ * each host send / recv vector), with the registration cache's holds on
+ * them (J->shold / rhold, released by mvxi_job_release); device vectors read
+ * MVX_BUF_DEVICE */
+static void packed_kinds(job_t *J, const tspan_t *T)
 {
+    unsigned long *mine[2 * MVX_MAXP];
+    int r, nmine = 0;
+    for (r = 0; r < J->nr; r++) {
+        J->shold[r] = J->rhold[r] = 0;
+        J->skind[r] = J->rkind[r] = MVX_BUF_DEVICE;
+        if (J->nsend[r] > 0 && !mvxi_is_device_ptr(J->send[r])) {
+            J->skind[r] = mvxi_buf_kind_hold(J->send[r] + T->lo, span_bytes(T, J->nsend[r]), &J->shold[r], mine, nmine);
+            if (J->shold[r]) mine[nmine++] = &J->shold[r];
+        }
+        if (J->nrecv[r] > 0 && !mvxi_is_device_ptr(J->recv[r])) {
+            J->rkind[r] = mvxi_buf_kind_hold(J->recv[r] + T->lo, span_bytes(T, J->nrecv[r]), &J->rhold[r], mine, nmine);
+            if (J->rhold[r]) mine[nmine++] = &J->rhold[r];
+        }
+    }
+    /* a span whose registration was merged into a later one's union and
+     * lost with it is asked again (as mvxi_job_kinds does) */
+    for (r = 0; r < J->nr; r++) {
+        if (J->skind[r] == MVX_BUF_PINNED && !J->shold[r] && mvx_host_pinned(J->send[r] + T->lo) != 1)
+            J->skind[r] = mvxi_buf_kind_hold(J->send[r] + T->lo, span_bytes(T, J->nsend[r]), &J->shold[r], NULL, 0);
+        if (J->rkind[r] == MVX_BUF_PINNED && !J->rhold[r] && mvx_host_pinned(J->recv[r] + T->lo) != 1)
+            J->rkind[r] = mvxi_buf_kind_hold(J->recv[r] + T->lo, span_bytes(T, J->nrecv[r]), &J->rhold[r], NULL, 0);
+    }
+    J->kinds = 1;
+}
+
+static int packed_setup(mvx_comm_t *c, job_t *J, const tspan_t *T, packed_bufs_t *B, hipStream_t st)
+{
+    mvx_work *w = mvxi_work(c);
     const int dt = J->P[0].dtype;
     size_t need = 0, off[4 * MVX_MAXP];
-    int r, rc;
+    int r, rc, bounce = 0;
+    if (!w) return MPI_ERR_INTERN;
+    packed_kinds(J, T);
     for (r = 0; r < J->nr; r++) {
-        const int sh = J->nsend[r] > 0 && !mvxi_is_device_ptr(J->send[r]);
-        const int rh = J->nrecv[r] > 0 && !mvxi_is_device_ptr(J->recv[r]);
+        const int sh = J->skind[r] != MVX_BUF_DEVICE, rh = J->rkind[r] != MVX_BUF_DEVICE;
         off[4 * r] = need;     need = al256(need + (sh ? span_bytes(T, J->nsend[r]) : 0));
         off[4 * r + 1] = need; need = al256(need + (size_t)(J->nsend[r] * T->size));
         off[4 * r + 2] = need; need = al256(need + (rh ? span_bytes(T, J->nrecv[r]) : 0));
         off[4 * r + 3] = need; need = al256(need + (size_t)(J->nrecv[r] * T->size));
         B->smir[r] = sh ? (char *)1 : NULL;
         B->rmir[r] = rh ? (char *)1 : NULL;
+        bounce |= (sh && mirror_bounced(J->skind[r], span_bytes(T, J->nsend[r]))) ||
+                  (rh && mirror_bounced(J->rkind[r], span_bytes(T, J->nrecv[r])));
     }
     if ((rc = mvxi_grow(&c->hpool, &c->hpool_bytes, need + 256))) return rc;
+    if (bounce && (rc = stage_init(&w->stage, MIRROR_CHUNK))) return rc;
     for (r = 0; r < J->nr; r++) {
         B->psend[r] = c->hpool + off[4 * r + 1];
         B->precv[r] = c->hpool + off[4 * r + 3];
         B->sorg[r] = J->send[r];
         B->rorg[r] = J->recv[r];
-        if (B->smir[r]) {
+        if (B->smir[r]) {      /* the send span into HBM (through the CPU where HIP may not copy it) */
             B->smir[r] = c->hpool + off[4 * r];
-            if (hipMemcpyAsync(B->smir[r], J->send[r] + T->lo, span_bytes(T, J->nsend[r]), hipMemcpyHostToDevice,
-                               st) != hipSuccess)
-                return MPI_ERR_OTHER;
+            if ((rc = mirror_in(&w->stage, B->smir[r], J->send[r] + T->lo, span_bytes(T, J->nsend[r]),
+                                J->skind[r], st)))
+                return rc;
             B->sorg[r] = B->smir[r] - T->lo;
         }
-        if (B->rmir[r]) {
+        if (B->rmir[r]) {      /* the recv span too: its bytes outside the type map go back as they were */
             B->rmir[r] = c->hpool + off[4 * r + 2];
-            if (hipMemcpyAsync(B->rmir[r], J->recv[r] + T->lo, span_bytes(T, J->nrecv[r]), hipMemcpyHostToDevice,
-                               st) != hipSuccess)
-                return MPI_ERR_OTHER;
+            if ((rc = mirror_in(&w->stage, B->rmir[r], J->recv[r] + T->lo, span_bytes(T, J->nrecv[r]),
+                                J->rkind[r], st)))
+                return rc;
             B->rorg[r] = B->rmir[r] - T->lo;
         }
         if (J->nsend[r] > 0 && (rc = mvx_type_pack(dt, B->sorg[r], B->psend[r], (size_t)J->nsend[r], st)))
@@ -444,34 +480,45 @@ static int packed_setup(mvx_comm_t *c, const job_t *J, const tspan_t *T, packed_
     return MPI_SUCCESS;
 }
 
-static int packed_finish(const job_t *J, const tspan_t *T, packed_bufs_t *B, hipStream_t st, int sync)
+static int packed_finish(mvx_comm_t *c, const job_t *J, const tspan_t *T, packed_bufs_t *B, hipStream_t st,
+                         int sync)
 {
+    mvx_work *w = mvxi_work(c);
     const int dt = J->P[0].dtype;
     int r, rc;
+    if (!w) return MPI_ERR_INTERN;
     for (r = 0; r < J->nr; r++) {
         if (J->nrecv[r] <= 0) continue;
         if ((rc = mvx_type_unpack(dt, B->precv[r], B->rorg[r], (size_t)J->nrecv[r], st))) return rc;
-        if (B->rmir[r] && hipMemcpyAsync(J->recv[r] + T->lo, B->rmir[r], span_bytes(T, J->nrecv[r]),
-                                         hipMemcpyDeviceToHost, st) != hipSuccess)
-            return MPI_ERR_OTHER;
+        if (B->rmir[r] && (rc = mirror_out(&w->stage, J->recv[r] + T->lo, B->rmir[r], span_bytes(T, J->nrecv[r]),
+                                           J->rkind[r], st)))
+            return rc;
     }
     return (sync && hipStreamSynchronize(st) != hipSuccess) ? MPI_ERR_OTHER : MPI_SUCCESS;
 }
 
-int mvxi_run_job_packed(mvx_comm_t *c, const job_t *J, hipStream_t st, int blocking)
+/* host vectors of a packed job (its spans are host memory) */
+int mvxi_job_packed_host(const job_t *J)
+{
+    int r, host = 0;
+    for (r = 0; r < J->nr; r++)
+        host |= (J->nsend[r] > 0 && !mvxi_is_device_ptr(J->send[r])) ||
+                (J->nrecv[r] > 0 && !mvxi_is_device_ptr(J->recv[r]));
+    return host;
+}
+
+int mvxi_run_job_packed(mvx_comm_t *c, job_t *J, hipStream_t st, int blocking)
 {
     mvx_work *w = mvxi_work(c);
     job_t *K;
     packed_bufs_t *B;
     tspan_t T;
-    int r, rc, host = 0;
+    int r, rc, host;
     if (!w) return MPI_ERR_INTERN;
     K = &w->pk_job;
     B = &w->pk_bufs;
     if ((rc = type_span(J->P[0].dtype, &T))) return rc;
-    for (r = 0; r < J->nr; r++)
-        host |= (J->nsend[r] > 0 && !mvxi_is_device_ptr(J->send[r])) ||
-                (J->nrecv[r] > 0 && !mvxi_is_device_ptr(J->recv[r]));
+    host = mvxi_job_packed_host(J);
     if (host && !blocking) return MPI_ERR_BUFFER;
     if ((rc = packed_setup(c, J, &T, B, st))) return rc;
     *K = *J;
@@ -480,7 +527,46 @@ int mvxi_run_job_packed(mvx_comm_t *c, const job_t *J, hipStream_t st, int block
         K->recv[r] = B->precv[r];
     }
     if ((rc = mvxi_run_device(c, K, st))) return rc;
-    return packed_finish(J, &T, B, st, blocking || host);
+    return packed_finish(c, J, &T, B, st, blocking || host);
+}
+
+/* dst = src, bytes of any kinds (MPIR_intra_Scan's self copy of a contiguous
+ * type when its op is undefined): device to device stream-ordered; with a
+ * host side the host side's kind is asked of the registration cache (held
+ * until the copy is done) and the copy is synchronous -- through the CPU
+ * where HIP may not copy the memory (MVX_BUF_BOUNCE) */
+int mvxi_copy_any(mvx_comm_t *c, void *dst, const void *src, size_t bytes, hipStream_t st, int sync)
+{
+    mvx_work *w = mvxi_work(c);
+    const int sdev = mvxi_is_device_ptr(src), ddev = mvxi_is_device_ptr(dst);
+    unsigned long hs = 0, hd = 0;
+    int ks = MVX_BUF_DEVICE, kd = MVX_BUF_DEVICE, rc = MPI_SUCCESS;
+    if (!bytes) return MPI_SUCCESS;
+    if (sdev && ddev) {
+        if (hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, st) != hipSuccess) return MPI_ERR_OTHER;
+        return (sync && hipStreamSynchronize(st) != hipSuccess) ? MPI_ERR_OTHER : MPI_SUCCESS;
+    }
+    if (!w) return MPI_ERR_INTERN;
+    if (!sdev) ks = mvxi_buf_kind_hold(src, bytes, &hs, NULL, 0);
+    if (!ddev) {
+        unsigned long *mine[1] = {&hs};
+        kd = mvxi_buf_kind_hold(dst, bytes, &hd, mine, hs ? 1 : 0);
+    }
+    if (!sdev && !ddev) {                       /* host to host: the CPU, after the stream */
+        if (hipStreamSynchronize(st) != hipSuccess) rc = MPI_ERR_OTHER;
+        else memmove(dst, src, bytes);
+    } else if ((ks == MVX_BUF_BOUNCE || kd == MVX_BUF_BOUNCE) && (rc = stage_init(&w->stage, MIRROR_CHUNK))) {
+        ;
+    } else if (!sdev) {
+        rc = mirror_in(&w->stage, (char *)dst, (const char *)src, bytes, ks, st);
+        if (!rc && hipStreamSynchronize(st) != hipSuccess) rc = MPI_ERR_OTHER;
+    } else {
+        rc = mirror_out(&w->stage, (char *)dst, (const char *)src, bytes, kd, st);   /* synchronises */
+    }
+    if (rc && hipDeviceSynchronize() != hipSuccess) (void)hipGetLastError();
+    mvxi_buf_release(hs);
+    mvxi_buf_release(hd);
+    return rc;
 }
 
 /* recvbuf = sendbuf over the type map (MPIR_intra_Scan's self copy when its
@@ -498,11 +584,17 @@ int mvxi_typed_copy(mvx_comm_t *c, int dt, long n, const char *send, char *recv,
     memset(P0, 0, sizeof *P0);
     P0->dtype = dt;
     K->nr = 1; K->P = P0; K->send[0] = send; K->recv[0] = recv; K->nsend[0] = n; K->nrecv[0] = n;
-    if ((rc = type_span(dt, &T)) || (rc = packed_setup(c, K, &T, B, st))) return rc;
+    K->kinds = 0;
+    if ((rc = type_span(dt, &T)) || (rc = packed_setup(c, K, &T, B, st))) {
+        mvxi_job_release(K, rc ? rc : MPI_ERR_OTHER);
+        return rc;
+    }
     if (n > 0 && hipMemcpyAsync(B->precv[0], B->psend[0], (size_t)(n * T.size), hipMemcpyDeviceToDevice, st) !=
                      hipSuccess)
-        return MPI_ERR_OTHER;
-    return packed_finish(K, &T, B, st, sync || B->smir[0] || B->rmir[0]);
+        rc = MPI_ERR_OTHER;
+    if (!rc) rc = packed_finish(c, K, &T, B, st, sync || B->smir[0] || B->rmir[0]);
+    mvxi_job_release(K, rc);
+    return rc;
 }
 
 /* ---- the slice schedule: large calls at p > 1, any buffer kind ----------

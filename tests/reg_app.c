@@ -34,6 +34,17 @@
  *                 itself (mvx_host_invalidate) while a call holds it: the
  *                 registration is deferred, not unpinned under the DMA, and
  *                 unregistered once the call is done.
+ *   reg_app shadow (GPU) buffers that share pages with a registration:
+ *                 (a) two adjacent 8 MiB heap buffers reduced together: the
+ *                 second's registration merges with the first's (which this
+ *                 same call holds) into one; (b) a thread reduces a 64 MiB
+ *                 heap buffer A over and over (the op holds A's
+ *                 registration) while the main thread runs a 2-rank
+ *                 Allreduce on a virtual communicator whose sendbuf starts
+ *                 in A's last page: when A is held that buffer is copied by
+ *                 the CPU (HIP refuses a copy that starts inside a
+ *                 registration and runs past it), else the two merge.  Every
+ *                 result bit-exact.
  * Prints "reg_app ok" and one JSON line of what it saw. */
 #define _GNU_SOURCE 1
 #include <malloc.h>
@@ -116,6 +127,19 @@ static int heap_pair(char **a, char **b, size_t n)
     return 1;
 }
 
+/* blocks of n1 and n2 bytes, the second starting in the first's last page */
+static int heap_adjacent(char **a, char **b, size_t n1, size_t n2)
+{
+    int t;
+    for (t = 0; t < 8; t++) {
+        *a = malloc(n1);
+        *b = malloc(n2);
+        if (*a && *b && ((uintptr_t)(*a + n1 - 1) & ~4095UL) == ((uintptr_t)*b & ~4095UL)) return 0;
+        if (!malloc(48)) return 1;                  /* shift the next pair (kept) */
+    }
+    return 1;
+}
+
 static int dry(void)
 {
     char *a, *b, *h, *m;
@@ -184,7 +208,7 @@ static int dry(void)
 static long deferred(void)
 {
     long d = -1;
-    mvx_host_register_deferred(&d, NULL, NULL);
+    mvx_host_register_deferred(&d, NULL, NULL, NULL);
     return d;
 }
 
@@ -197,7 +221,7 @@ static int stub(void)
     reg0 = n_reg;
     CHECK(mvx_host_register(a, 8 * MIB) == 0 && entries() == 1 && n_reg == reg0 + 1, "register through the stub");
     unreg0 = n_unreg;
-    mvx_host_register_deferred(NULL, NULL, &u0);
+    mvx_host_register_deferred(NULL, NULL, &u0, NULL);
     in_hook_probe = 1;
     free(a);                                        /* the hook: no HIP call */
     in_hook_probe = 0;
@@ -211,7 +235,7 @@ static int stub(void)
     mvx_host_invalidate(m, 4 * MIB);                /* a host MPI's hook: nothing left to drop */
     in_hook_probe = 0;
     CHECK(hip_in_release == 0 && deferred() == 1 && n_unreg == unreg0 + 1, "munmap only defers");
-    mvx_host_register_deferred(NULL, NULL, &u1);
+    mvx_host_register_deferred(NULL, NULL, &u1, NULL);
     CHECK(u1 == u0 + 1, "counter agrees");
     mvx_host_register_enable(0, 0);                 /* off: flushes */
     CHECK(n_unreg == unreg0 + 2 && deferred() == 0, "off unregisters the rest");
@@ -372,7 +396,7 @@ static void *inval_worker(void *arg)
     while (!nb_go) ;
     clock_gettime(CLOCK_MONOTONIC, &t0);
     for (i = 0; held < 1; i++) {
-        mvx_host_register_deferred(NULL, &held, NULL);
+        mvx_host_register_deferred(NULL, &held, NULL, NULL);
         clock_gettime(CLOCK_MONOTONIC, &t);
         if (t.tv_sec - t0.tv_sec > 20) break;
     }
@@ -416,14 +440,14 @@ static int neighbour(void)
     CHECK(entries() == 2 && hits1 - hits0 == 48, "every call found both registrations");
 
     /* a release of x itself reported while a call holds it */
-    mvx_host_register_deferred(&d0, NULL, &u0);
+    mvx_host_register_deferred(&d0, NULL, &u0, NULL);
     nb_inval = x;
     nb_bytes = nb;
     CHECK(pthread_create(&th, NULL, inval_worker, NULL) == 0, "thread 2");
     nb_go = 1;
     CHECK(sum_check(x, y, n, 999) == 0, "bit-exact with the release deferred under it");
     pthread_join(th, NULL);
-    mvx_host_register_deferred(&d1, &held_after, &u1);
+    mvx_host_register_deferred(&d1, &held_after, &u1, NULL);
     CHECK(nb_held_seen >= 1, "the release came while the call held the registration");
     CHECK(d1 == 0 && held_after == 0 && u1 >= u0 + 1, "unregistered once the call was done");
     CHECK(entries() == 1, "y stays registered");
@@ -435,6 +459,95 @@ static int neighbour(void)
     free(x);
     free(y);
     CHECK(entries() == 0, "frees dropped the registrations");
+    return 0;
+}
+
+/* ---- buffers under a neighbour's registration (GPU) ------------------- */
+static volatile int sh_stop;
+static float *sh_a, *sh_c;
+static size_t sh_n;
+static long sh_iters, sh_bad;
+
+static void *sh_worker(void *arg)
+{
+    int len = (int)sh_n;
+    MPI_Datatype t = MPI_FLOAT;
+    (void)arg;
+    while (!sh_stop) {
+        MPIR_SUM(sh_a, sh_c, &len, &t);          /* c += a: holds A's registration while it runs */
+        if (mvx_op_errno() != 0) sh_bad++;
+        sh_iters++;
+    }
+    return NULL;
+}
+
+static int shadow(void)
+{
+    const size_t nb8 = 8 * MIB, n8 = nb8 / sizeof(float), nb = 64 * MIB, n = nb / sizeof(float);
+    float *x, *y, *c0, *b2, *r1, *r2;
+    char *pa, *pb;
+    long bounced0, bounced1, calls = 0;
+    MPI_Comm comm;
+    pthread_t th;
+    size_t i;
+    int rep;
+    mallopt(M_MMAP_THRESHOLD, 512 * MIB);
+    mallopt(M_TRIM_THRESHOLD, 1024 * MIB);
+
+    /* (a) the call's own operands sharing a page */
+    CHECK(heap_adjacent(&pa, &pb, nb8, nb8) == 0, "adjacent pair");
+    x = (float *)pa;
+    y = (float *)pb;
+    CHECK(((uintptr_t)((char *)x + nb8 - 1) & ~4095UL) == ((uintptr_t)y & ~4095UL), "x and y share a page");
+    CHECK(sum_check(x, y, n8, 21) == 0, "adjacent operands, one call");
+    CHECK(entries() == 1, "their registrations merged into one");
+    CHECK(sum_check(x, y, n8, 22) == 0, "again, on the merged registration");
+    free(x);
+    free(y);
+    CHECK(entries() == 0, "freed");
+
+    /* (b) a neighbour of a registration another call holds */
+    CHECK(heap_adjacent(&pa, &pb, nb, nb8) == 0, "B starts in A's last page");
+    if (!malloc(3 * 4096)) return 1;
+    sh_a = (float *)pa;
+    sh_n = n;
+    sh_c = malloc(nb);
+    c0 = malloc(nb);
+    b2 = malloc(nb8 + 3 * 4096);
+    r1 = malloc(nb8 + 3 * 4096);
+    r2 = malloc(nb8 + 3 * 4096);
+    CHECK(sh_c && c0 && b2 && r1 && r2, "malloc");
+    fill(sh_a, n, 31);
+    fill(c0, n, 32);
+    memcpy(sh_c, c0, nb);
+    fill((float *)pb, n8, 33);
+    fill(b2, n8, 34);
+    CHECK(mvx_comm_init_local(&comm, 2, 0) == 0, "virtual communicator");
+    mvx_host_register_deferred(NULL, NULL, NULL, &bounced0);
+    CHECK(pthread_create(&th, NULL, sh_worker, NULL) == 0, "thread");
+    for (rep = 0; rep < 40; rep++) {
+        void *s[2] = {pb, b2}, *r[2] = {r1, r2};
+        int rcs[2] = {-1, -1};
+        memset(r1, 0, nb8);
+        memset(r2, 0, nb8);
+        CHECK(mvx_allreduce_multi(s, r, (int)n8, MPI_FLOAT, MPI_SUM, comm, rcs, NULL) == 0 && rcs[0] == 0 &&
+              rcs[1] == 0, "allreduce");
+        for (i = 0; i < n8; i++)
+            if (r1[i] != ((float *)pb)[i] + b2[i] || r2[i] != r1[i]) break;
+        CHECK(i == n8, "bit-exact beside a held registration");
+        calls++;
+    }
+    sh_stop = 1;
+    pthread_join(th, NULL);
+    mvx_host_register_deferred(NULL, NULL, NULL, &bounced1);
+    CHECK(sh_bad == 0, "the op thread's calls");
+    for (i = 0; i < n; i++)
+        if (sh_c[i] != c0[i] + (float)sh_iters * sh_a[i]) break;
+    CHECK(i == n, "the op thread's result");
+    printf("{\"mode\": \"shadow\", \"allreduce_calls\": %ld, \"op_calls\": %ld, \"bounced\": %ld}\n", calls,
+           sh_iters, bounced1 - bounced0);
+    mvx_comm_free(&comm);
+    free(pa); free(pb); free(sh_c); free(c0); free(b2); free(r1); free(r2);
     return 0;
 }
 
@@ -451,7 +564,7 @@ int main(int argc, char **argv)
         return 1;
     }
     rc = !strcmp(argv[1], "dry") ? dry() : !strcmp(argv[1], "gpu") ? gpu() : !strcmp(argv[1], "stress") ? stress()
-       : !strcmp(argv[1], "neighbour") ? neighbour()
+       : !strcmp(argv[1], "neighbour") ? neighbour() : !strcmp(argv[1], "shadow") ? shadow()
 #ifdef REG_STUB
        : !strcmp(argv[1], "stub") ? stub()
 #endif

@@ -126,6 +126,67 @@ def test_neighbour_frees_and_deferred_release_under_dma():
     print(p.stdout)
 
 
+def test_buffers_under_a_neighbours_registration():
+    """tests/reg_app.c shadow: HIP refuses a copy that starts inside a
+    registration and runs past it (tools/shadow_probe.c), so a buffer whose
+    first page another buffer's registration covers is merged with it (the
+    same call's operands: one registration) or, while another call holds that
+    registration, copied by the CPU -- a 2-rank Allreduce on a virtual
+    communicator beside a thread that keeps reducing the neighbour.  Every
+    result bit-exact."""
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    out = os.path.join(tempfile.mkdtemp(prefix="mvx_reg_"), "reg_app")
+    pkg = os.path.join(root, "mvapich-cce_amd")
+    subprocess.check_call(["gcc", "-O2", "-std=gnu99", "-Wall", "-Werror", "-D__HIP_PLATFORM_AMD__",
+                           "-I/opt/rocm/include", "-I" + os.path.join(root, "include"),
+                           os.path.join(here, "reg_app.c"), "-o", out, "-L" + pkg, "-lmvx",
+                           "-L/opt/rocm/lib", "-lamdhip64", "-lpthread", "-Wl,-rpath," + pkg,
+                           "-Wl,-rpath,/opt/rocm/lib"])
+    env = {k: v for k, v in os.environ.items() if not k.startswith("MVX_HOST_REGISTER")}
+    p = subprocess.run([out, "shadow"], capture_output=True, text=True, timeout=180, env=env)
+    assert p.returncode == 0 and "reg_app ok" in p.stdout, p.stdout[-2000:] + p.stderr[-2000:]
+    print(p.stdout)
+
+
+def test_adjacent_operands_share_a_registration(mvx):
+    """Mode 2 (this process): two 8 MiB heap buffers, the second starting in
+    the first's last page, reduced by one op call -- the first's registration
+    (held by the call) merges with the second's into one, no HIP copy refused,
+    bit-exact; then unregistered before the frees."""
+    libc = ctypes.CDLL("libc.so.6")
+    libc.malloc.restype = ctypes.c_void_p
+    libc.malloc.argtypes = [ctypes.c_size_t]
+    libc.free.argtypes = [ctypes.c_void_p]
+    libc.mallopt.argtypes = [ctypes.c_int, ctypes.c_int]
+    libc.mallopt(-3, 512 * MIB)               # M_MMAP_THRESHOLD: from the heap
+    libc.mallopt(-1, 1024 * MIB)              # M_TRIM_THRESHOLD
+    n = 8 * MIB // 4
+    try:
+        for _ in range(8):
+            px, py = libc.malloc(n * 4), libc.malloc(n * 4)
+            if (px + n * 4 - 1) // 4096 == py // 4096:
+                break
+            libc.malloc(48)
+    finally:
+        libc.mallopt(-3, 128 * 1024)          # glibc's defaults again
+        libc.mallopt(-1, 128 * 1024)
+    assert (px + n * 4 - 1) // 4096 == py // 4096
+    x, y = _as_array(px, n), _as_array(py, n)
+    rng = np.random.default_rng(3)
+    x[:] = rng.integers(-8, 8, n).astype(np.float32)
+    y[:] = rng.integers(-8, 8, n).astype(np.float32)
+    want = x + y
+    _sum_call(mvx, px, py, n)
+    ok = bool(np.array_equal(y, want))
+    st = mvx.host_register_stats()
+    mvx.host_unregister(px)
+    mvx.host_unregister(py)
+    libc.free(px)
+    libc.free(py)
+    assert ok and st["entries"] == 1, st
+
+
 def test_free_and_reallocate_same_size(mvx):
     """Mode 2 (this process's contract): a registered buffer is
     unregistered, freed and the same size allocated again (the same address
