@@ -690,6 +690,7 @@ template <> __device__ inline void set_unit<8>(pu32x4 &v, int g, pu32x2 x)
     v[2 * g] = x.x;
     v[2 * g + 1] = x.y;
 }
+template <> __device__ inline void set_unit<16>(pu32x4 &v, int, pu32x4 x) { v = x; }
 template <> __device__ inline void set_unit<4>(pu32x4 &v, int g, uint32_t x) { v[g] = x; }
 template <> __device__ inline void set_unit<2>(pu32x4 &v, int g, uint16_t x)
 {
@@ -702,16 +703,22 @@ template <> __device__ inline void set_unit<1>(pu32x4 &v, int g, uint8_t x)
     v[g >> 2] = (v[g >> 2] & ~(0xffu << s)) | ((uint32_t)x << s);
 }
 
-template <int W, int TILE>
+// The unit offsets come from LDS (LDSU, up to MERGE_UNITS_LDS units per
+// element) or from global memory: a template argument, not a run-time
+// select -- a select between the two made the compiler address both through
+// flat loads and stores in the inner loop.  Units outside the tile go to a
+// trash word past its end (a select on the LDS address, no branch), and the
+// hull's two edge words are stored byte by byte, so every unit of the tile
+// is one LDS store.
+template <int W, int TILE, bool LDSU>
 __global__ void __launch_bounds__(256)
 k_unpack_merge(const char *__restrict__ packed, char *__restrict__ dst, const int *__restrict__ uoff, long upe,
                long n, long ext, long lo, long hi, uintptr_t a0, uintptr_t h0, uintptr_t h1)
 {
     typedef typename UnitT<W>::t V;
-    __shared__ pu32x4 s_tile[TILE / 16];
-    __shared__ int s_uoff[MERGE_UNITS_LDS];
-    const bool lds_units = upe <= MERGE_UNITS_LDS;
-    if (lds_units)
+    __shared__ pu32x4 s_tile[TILE / 16 + 1];            // + the trash word
+    __shared__ int s_uoff[LDSU ? MERGE_UNITS_LDS : 1];
+    if (LDSU)
         for (int u = threadIdx.x; u < (int)upe; u += 256) s_uoff[u] = uoff[u];
     const uintptr_t t0 = a0 + (uintptr_t)blockIdx.x * TILE;                // this tile's first word
     const uintptr_t tend = t0 + TILE < ((h1 + 15) & ~(uintptr_t)15) ? t0 + TILE
@@ -734,9 +741,6 @@ k_unpack_merge(const char *__restrict__ packed, char *__restrict__ dst, const in
     const int up = (int)upe, ext32 = (int)ext, span = (int)(tend - t0);
     const int e0 = (int)(ilo * ext - a);
     const long q0 = ilo * upe, qn = n * upe, c0 = q0 / G, c1 = (ihi * upe + G - 1) / G;
-    // the words of the tile wholly inside the hull [h0, h1), tile-relative
-    const long hl = (long)(h0 - t0), hh = (long)(h1 - t0);
-    const int in_lo = hl < 0 ? 0 : (int)hl, in_hi = hh > span ? span : (int)hh;
     for (long c = c0 + threadIdx.x; c < c1; c += 512) {
         pu32x4 v[2];
 #pragma unroll
@@ -748,29 +752,40 @@ k_unpack_merge(const char *__restrict__ packed, char *__restrict__ dst, const in
         for (int u = 0; u < 2; ++u) {
             const long cc = c + 256 * u;
             if (cc >= c1) continue;
-            const bool whole = (cc + 1) * G <= qn;
-            long q = cc * G;
-            const int qr = (int)(q - q0);          // > -G: the first chunk may start in element ilo - 1
-            int ir = qr >= 0 ? qr / up : -1, j = qr >= 0 ? qr - ir * up : up + qr;
+            const int valid = qn - cc * G < G ? (int)(qn - cc * G) : G;   // units of the chunk in the stream
+            if (valid < G) {                       // the stream's last, partial chunk: unit by unit
+                v[u] = pu32x4{0, 0, 0, 0};
+                for (int g = 0; g < valid; ++g) set_unit<W>(v[u], g, *(const V *)(packed + (cc * G + g) * W));
+            }
+            // > -G: the first chunk may start in elements before ilo (several
+            // when an element has fewer than G units), whose units all land
+            // below the tile (ilo is the first element reaching it); ir is
+            // the floor of qr / up, so j is a unit index in every case
+            const int qr = (int)(cc * G - q0);
+            int ir = qr >= 0 ? (int)((unsigned)qr / (unsigned)up) : -(int)((unsigned)(up - 1 - qr) / (unsigned)up);
+            int j = qr - ir * up;
+            int rel[G];
 #pragma unroll
-            for (int g = 0; g < G; ++g, ++q) {
-                if (q < qn && ir >= 0) {
-                    const int rel = ir * ext32 + e0 + (lds_units ? s_uoff[j] : uoff[j]);
-                    if ((unsigned)rel < (unsigned)span) {
-                        const V x = whole ? unit_of<W>(v[u], g) : *(const V *)(packed + q * W);
-                        const int word = rel & ~15;
-                        if (word < in_lo || word + 16 > in_hi) *(V *)(t0 + (uintptr_t)rel) = x;   // past the hull: units only
-                        else *(V *)((char *)s_tile + rel) = x;
-                    }
-                }
+            for (int g = 0; g < G; ++g) {
+                rel[g] = ir * ext32 + e0 + (LDSU ? s_uoff[j] : uoff[j]);
                 if (++j == up) { j = 0; ++ir; }
+            }
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                const bool in = (g < valid) & ((unsigned)rel[g] < (unsigned)span);
+                *(V *)((char *)s_tile + (in ? rel[g] : TILE)) = unit_of<W>(v[u], g);
             }
         }
     }
     __syncthreads();
     for (int w = threadIdx.x; w < nw; w += 256) {
         const uintptr_t at = t0 + 16 * (uintptr_t)w;
-        if (at >= h0 && at + 16 <= h1) __builtin_nontemporal_store(s_tile[w], (pu32x4 *)at);
+        if (at >= h0 && at + 16 <= h1) {
+            __builtin_nontemporal_store(s_tile[w], (pu32x4 *)at);
+        } else {                                   // an edge word of the hull: its hull bytes only
+            const uintptr_t b0 = at > h0 ? at : h0, b1 = at + 16 < h1 ? at + 16 : h1;
+            for (uintptr_t b = b0; b < b1; ++b) *(char *)b = ((const char *)s_tile)[16 * w + (b - at)];
+        }
     }
 }
 
@@ -837,13 +852,20 @@ static int launch_merge(Type &t, int wi, const void *src, void *dst, long count,
         const char *e = getenv("MVX_UNPACK_TILE_KIB");
         TILE = e && atoi(e) == 16 ? 16384 : MERGE_TILE;
     }
-    const long tiles = (long)((((h1 + 15) & ~(uintptr_t)15) - a0 + TILE - 1) / TILE);
+    // (the 16 KiB tuning tile only with the unit offsets in LDS)
+    const long T = upe > MERGE_UNITS_LDS ? MERGE_TILE : TILE;
+    const long tiles = (long)((((h1 + 15) & ~(uintptr_t)15) - a0 + T - 1) / T);
     if (tiles < 1 || tiles > INT32_MAX) return MPI_ERR_OTHER;
-    if (TILE == 16384)
-        hipLaunchKernelGGL((k_unpack_merge<W, 16384>), dim3((unsigned)tiles), dim3(256), 0, st, (const char *)src,
-                           (char *)dst, (const int *)t.dunits[wi], upe, count, t.extent, lo, hi, a0, h0, h1);
+    if (upe > MERGE_UNITS_LDS)
+        hipLaunchKernelGGL((k_unpack_merge<W, MERGE_TILE, false>), dim3((unsigned)tiles), dim3(256), 0, st,
+                           (const char *)src, (char *)dst, (const int *)t.dunits[wi], upe, count, t.extent, lo, hi,
+                           a0, h0, h1);
+    else if (TILE == 16384)
+        hipLaunchKernelGGL((k_unpack_merge<W, 16384, true>), dim3((unsigned)tiles), dim3(256), 0, st,
+                           (const char *)src, (char *)dst, (const int *)t.dunits[wi], upe, count, t.extent, lo, hi,
+                           a0, h0, h1);
     else
-        hipLaunchKernelGGL((k_unpack_merge<W, MERGE_TILE>), dim3((unsigned)tiles), dim3(256), 0, st,
+        hipLaunchKernelGGL((k_unpack_merge<W, MERGE_TILE, true>), dim3((unsigned)tiles), dim3(256), 0, st,
                            (const char *)src, (char *)dst, (const int *)t.dunits[wi], upe, count, t.extent, lo, hi,
                            a0, h0, h1);
     return hipGetLastError() == hipSuccess ? MPI_SUCCESS : MPI_ERR_OTHER;
@@ -863,7 +885,7 @@ static int launch_merge(Type &t, int wi, const void *src, void *dst, long count,
 // needs only 16-byte tile starts; pack_ept makes them 64-byte ones.)
 #define PACK_TILE 8192               // LDS bytes of extent layout per workgroup
 
-template <int W, int TILE>
+template <int W, int TILE, bool LDSU>
 __global__ void __launch_bounds__(256)
 k_pack_tiles(const char *__restrict__ src, char *__restrict__ dst, const int *__restrict__ uoff, long upe, long n,
              long ext, long lo, long hi, long ept)
@@ -871,9 +893,8 @@ k_pack_tiles(const char *__restrict__ src, char *__restrict__ dst, const int *__
     typedef typename UnitT<W>::t V;
     constexpr int G = 16 / W;
     __shared__ pu32x4 s_tile[TILE / 16];
-    __shared__ int s_uoff[MERGE_UNITS_LDS];
-    const bool lds_units = upe <= MERGE_UNITS_LDS;
-    if (lds_units)
+    __shared__ int s_uoff[LDSU ? MERGE_UNITS_LDS : 1];   // LDSU: as in k_unpack_merge
+    if (LDSU)
         for (int u = threadIdx.x; u < (int)upe; u += 256) s_uoff[u] = uoff[u];
     const long i0 = (long)blockIdx.x * ept;
     const long i1 = i0 + ept < n ? i0 + ept : n;
@@ -890,20 +911,20 @@ k_pack_tiles(const char *__restrict__ src, char *__restrict__ dst, const int *__
     const int up = (int)upe, ext32 = (int)ext;
     const int e0 = (int)(i0 * ext - (long)(a0 - (uintptr_t)src));
     for (long c = c0 + threadIdx.x; c < c1; c += 256) {
-        const int qr = (int)(c * G - qlo);
-        int ir = qr / up, j = qr - ir * up;
+        const unsigned qr = (unsigned)(c * G - qlo);
+        int ir = (int)(qr / (unsigned)up), j = (int)qr - ir * up;
         if ((c + 1) * G <= qn) {
             pu32x4 out = {0, 0, 0, 0};
 #pragma unroll
             for (int g = 0; g < G; ++g) {
-                const int rel = ir * ext32 + e0 + (lds_units ? s_uoff[j] : uoff[j]);
+                const int rel = ir * ext32 + e0 + (LDSU ? s_uoff[j] : uoff[j]);
                 set_unit<W>(out, g, *(const V *)((const char *)s_tile + rel));
                 if (++j == up) { j = 0; ++ir; }
             }
             __builtin_nontemporal_store(out, (pu32x4 *)(dst + 16 * c));
         } else {
             for (long q = c * G; q < qn; ++q) {
-                const int rel = ir * ext32 + e0 + (lds_units ? s_uoff[j] : uoff[j]);
+                const int rel = ir * ext32 + e0 + (LDSU ? s_uoff[j] : uoff[j]);
                 *(V *)(dst + q * W) = *(const V *)((const char *)s_tile + rel);
                 if (++j == up) { j = 0; ++ir; }
             }
@@ -961,12 +982,18 @@ static int launch_tiles(Type &t, int wi, const void *src, void *dst, long count,
 {
     const long tiles = (count + ept - 1) / ept;
     if (tiles < 1 || tiles > INT32_MAX) return MPI_ERR_OTHER;
-    if (pack_tile_bytes() == 16384)
-        hipLaunchKernelGGL((k_pack_tiles<W, 16384>), dim3((unsigned)tiles), dim3(256), 0, st, (const char *)src,
-                           (char *)dst, (const int *)t.dunits[wi], t.units[wi], count, t.extent, lo, hi, ept);
-    else
-        hipLaunchKernelGGL((k_pack_tiles<W, PACK_TILE>), dim3((unsigned)tiles), dim3(256), 0, st, (const char *)src,
-                           (char *)dst, (const int *)t.dunits[wi], t.units[wi], count, t.extent, lo, hi, ept);
+#define MVX_PACK_TILES_LAUNCH(TL, LU)                                                                            \
+    hipLaunchKernelGGL((k_pack_tiles<W, TL, LU>), dim3((unsigned)tiles), dim3(256), 0, st, (const char *)src,      \
+                       (char *)dst, (const int *)t.dunits[wi], t.units[wi], count, t.extent, lo, hi, ept)
+    const bool lu = t.units[wi] <= MERGE_UNITS_LDS;
+    if (pack_tile_bytes() == 16384) {
+        if (lu) MVX_PACK_TILES_LAUNCH(16384, true);
+        else MVX_PACK_TILES_LAUNCH(16384, false);
+    } else {
+        if (lu) MVX_PACK_TILES_LAUNCH(PACK_TILE, true);
+        else MVX_PACK_TILES_LAUNCH(PACK_TILE, false);
+    }
+#undef MVX_PACK_TILES_LAUNCH
     return hipGetLastError() == hipSuccess ? MPI_SUCCESS : MPI_ERR_OTHER;
 }
 
