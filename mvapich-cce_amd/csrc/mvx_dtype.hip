@@ -578,15 +578,19 @@ k_pack_units(const char *__restrict__ src, char *__restrict__ dst, const int *__
     long i = q / upe, j = q - i * upe;
     long ix = i * extent;                         // i * extent, carried
     while (q < N) {
+        // (a flag per unit, not a null destination: a pointer that may be
+        // null was addressed through flat stores, each waiting for every load)
         V v[U];
-        char *to[U];
+        long to[U];
+        bool ok[U];
 #pragma unroll
         for (int k = 0; k < U; ++k) {
-            to[k] = nullptr;
-            if (q < N) {
+            ok[k] = q < N;
+            to[k] = 0;
+            if (ok[k]) {
                 const long e = ix + (LDS ? s_uoff[j] : uoff[j]);
                 const char *from = PACK ? src + e : src + q * W;
-                to[k] = PACK ? dst + q * W : dst + e;
+                to[k] = PACK ? q * W : e;
                 v[k] = __builtin_nontemporal_load((const V *)from);
             }
             q += T;
@@ -596,7 +600,7 @@ k_pack_units(const char *__restrict__ src, char *__restrict__ dst, const int *__
         }
 #pragma unroll
         for (int k = 0; k < U; ++k)
-            if (to[k]) __builtin_nontemporal_store(v[k], (V *)to[k]);
+            if (ok[k]) __builtin_nontemporal_store(v[k], (V *)(dst + to[k]));
     }
 }
 
