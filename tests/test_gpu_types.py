@@ -369,3 +369,92 @@ def test_whole_word_unpack_keeps_every_other_byte(mvx, oracle):
         for h in made:
             mvx.MPI_Type_free(h)
             oracle.type_free(h)
+
+
+def _random_type(mvx, oracle, rng):
+    """A random hindexed / struct type of 1-, 2-, 4- and 8-byte pieces:
+    blocks in random order (the type map's order is the packed order),
+    gaps, sometimes reaching below the origin, sometimes nested in an
+    hvector whose stride leaves a gap.  Returns the handles to free."""
+    base = [(C, 1), (B, 1), (4, 2), (I, 4), (F, 4), (D, 8)]
+    nb = int(rng.integers(1, 6))
+    kind = "struct" if rng.random() < 0.4 else "hindexed"
+    if kind == "hindexed":
+        bt, bs = base[int(rng.integers(len(base)))]
+        types = [bt] * nb
+        sizes = [bs] * nb
+    else:
+        pick = [base[int(i)] for i in rng.integers(len(base), size=nb)]
+        types = [p[0] for p in pick]
+        sizes = [p[1] for p in pick]
+    lens = [int(x) for x in rng.integers(1, 5, size=nb)]
+    displs, cur = [], 0
+    for s, ln in zip(sizes, lens):
+        cur += int(rng.integers(0, 4)) * s          # a gap of whole pieces
+        cur = (cur + s - 1) // s * s
+        displs.append(cur)
+        cur += s * ln
+    if rng.random() < 0.25:                         # reach below the origin
+        shift = 8 * int(rng.integers(1, 4))
+        displs = [d - shift for d in displs]
+    order = rng.permutation(nb)
+    displs = [displs[i] for i in order]
+    lens = [lens[i] for i in order]
+    types = [types[i] for i in order]
+    if kind == "hindexed":
+        h = _both(mvx, oracle, "hindexed", nb, lens, displs, types[0])
+    else:
+        h = _both(mvx, oracle, "struct", nb, lens, displs, types)
+    made = [h]
+    if rng.random() < 0.3:
+        ext = mvx.MPI_Type_extent(h)[1]
+        stride = ext + 8 * int(rng.integers(0, 3))
+        h = _both(mvx, oracle, "hvector", int(rng.integers(2, 4)), 1, stride, h)
+        made.append(h)
+    return h, made
+
+
+@pytest.mark.parametrize("batch", range(8))
+def test_random_type_maps_pack_unpack(mvx, oracle, batch):
+    """Seeded random type maps (_random_type) through every pack / unpack
+    kernel the dispatch picks -- the tiled pack and whole-word unpack
+    (16-byte-aligned packed buffer), the unit kernel and the piece kernel
+    (packed buffer 4 bytes off) -- at counts 1 to 65537 and a random origin
+    phase: the packed streams agree, and unpack(pack(x)) into a patterned
+    buffer with guard bands equals the oracle's type-map copy (type-map bytes
+    land, holes and guards keep their pattern)."""
+    import torch
+    rng = np.random.default_rng(4242 + batch)
+    for _ in range(15):
+        h, made = _random_type(mvx, oracle, rng)
+        try:
+            ext = mvx.MPI_Type_extent(h)[1]
+            size = mvx.MPI_Type_size(h)[1]
+            L = mvx.type_layout(h)
+            for n in (1, 2, 17, 1000, 65537):
+                phase = int(rng.integers(0, 16))
+                guard = 256
+                off = guard + phase - min(0, L["span_lo"])
+                nb = off + (n - 1) * ext + L["span_hi"] + guard
+                x = rng.integers(0, 256, nb, dtype=np.uint8)
+                y0 = rng.integers(0, 256, nb, dtype=np.uint8)
+                dx = torch.from_numpy(x).cuda()
+                dy = torch.from_numpy(y0).cuda()
+                dp = torch.zeros(max(n * size, 16), dtype=torch.uint8, device="cuda")
+                dq = torch.zeros(max(n * size, 16) + 16, dtype=torch.uint8, device="cuda")
+                assert mvx.type_pack(h, dx.data_ptr() + off, dp, n) == 0
+                assert mvx.type_pack(h, dx.data_ptr() + off, dq.data_ptr() + 4, n) == 0
+                assert torch.equal(dq[4:4 + n * size], dp[:n * size]), (h, n, phase)
+                assert mvx.type_unpack(h, dp, dy.data_ptr() + off, n) == 0
+                ref = y0.copy()
+                assert oracle.type_copy(ref[off:], x[off:], n, h) == 0
+                got = T.from_dev(dy)
+                assert np.array_equal(got, ref), (L, n, phase, np.flatnonzero(got != ref)[:8])
+                # and from the misaligned packed copy (unit / piece kernels)
+                dz = torch.from_numpy(y0).cuda()
+                assert mvx.type_unpack(h, dq.data_ptr() + 4, dz.data_ptr() + off, n) == 0
+                assert np.array_equal(T.from_dev(dz), ref), (L, n, phase, "misaligned packed")
+        finally:
+            for m in reversed(made):
+                mvx.MPI_Type_free(m)
+                oracle.type_free(m)
