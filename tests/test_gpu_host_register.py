@@ -150,41 +150,34 @@ def test_buffers_under_a_neighbours_registration():
 
 
 def test_adjacent_operands_share_a_registration(mvx):
-    """Mode 2 (this process): two 8 MiB heap buffers, the second starting in
-    the first's last page, reduced by one op call -- the first's registration
-    (held by the call) merges with the second's into one, no HIP copy refused,
-    bit-exact; then unregistered before the frees."""
+    """Mode 2 (this process): two 8 MiB host operands, the second starting in
+    the first's last page (carved from one malloc'd block, as back-to-back
+    heap chunks lie), reduced by one op call -- the first's registration (held
+    by the call) merges with the second's into one, no HIP copy refused,
+    bit-exact; then unregistered before the free."""
     libc = ctypes.CDLL("libc.so.6")
     libc.malloc.restype = ctypes.c_void_p
     libc.malloc.argtypes = [ctypes.c_size_t]
     libc.free.argtypes = [ctypes.c_void_p]
-    libc.mallopt.argtypes = [ctypes.c_int, ctypes.c_int]
-    libc.mallopt(-3, 512 * MIB)               # M_MMAP_THRESHOLD: from the heap
-    libc.mallopt(-1, 1024 * MIB)              # M_TRIM_THRESHOLD
     n = 8 * MIB // 4
-    try:
-        for _ in range(8):
-            px, py = libc.malloc(n * 4), libc.malloc(n * 4)
-            if (px + n * 4 - 1) // 4096 == py // 4096:
-                break
-            libc.malloc(48)
-    finally:
-        libc.mallopt(-3, 128 * 1024)          # glibc's defaults again
-        libc.mallopt(-1, 128 * 1024)
+    base = libc.malloc(2 * n * 4 + 3 * 4096)
+    assert base
+    px = (base + 4095) // 4096 * 4096 + 64    # x ends 64 bytes into a page
+    py = px + n * 4 + 16                      # y starts 16 bytes later, same page
     assert (px + n * 4 - 1) // 4096 == py // 4096
     x, y = _as_array(px, n), _as_array(py, n)
     rng = np.random.default_rng(3)
     x[:] = rng.integers(-8, 8, n).astype(np.float32)
     y[:] = rng.integers(-8, 8, n).astype(np.float32)
     want = x + y
+    st0 = mvx.host_register_stats()
     _sum_call(mvx, px, py, n)
     ok = bool(np.array_equal(y, want))
     st = mvx.host_register_stats()
     mvx.host_unregister(px)
     mvx.host_unregister(py)
-    libc.free(px)
-    libc.free(py)
-    assert ok and st["entries"] == 1, st
+    libc.free(base)
+    assert ok and st["entries"] - st0["entries"] == 1, (st0, st)
 
 
 def test_free_and_reallocate_same_size(mvx):
