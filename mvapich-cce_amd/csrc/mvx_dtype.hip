@@ -56,6 +56,10 @@ struct Type {
     // only)
     int *dunits[5];
     long units[5];
+    // after the units in dunits[w] (W <= 8): the offsets of the G = 16 / W
+    // units of a 16-byte packed chunk, per chunk phase -- tabP[w] phases
+    // (a period of tabP chunks holds whole elements), 0: no table
+    long tabP[5];
     // whole-word unpack (merge_ok): 0 not decided, 1 yes, -1 no; the map's
     // reach [mlo, mhi) around the element origin
     int merge;
@@ -559,6 +563,7 @@ template <> struct UnitT<8> { typedef pu32x2 t; };
 template <> struct UnitT<16> { typedef pu32x4 t; };
 
 #define UNITS_LDS 2048   // unit tables this small are read from LDS
+#define CHUNK_TAB_MAX 2048   // chunk tables (Type::tabP) up to this many entries
 
 template <bool PACK, int W, int U, bool LDS>
 __global__ void __launch_bounds__(256)
@@ -618,6 +623,21 @@ static bool unit_table(Type &t, int W, int wi)
         for (long o = 0; o < m.len; o += W) u.push_back((int)(m.off + o));
     }
     if (!ok || u.empty()) { t.units[wi] = -1; return false; }
+    const long upe = (long)u.size();
+    t.tabP[wi] = 0;
+    if (W <= 8) {
+        // chunk c, unit g: unit q = c G + g of the stream; with c = k P + p,
+        // its element is k EPP + (p G + g) / upe and its offset in that
+        // element u[(p G + g) % upe] (EPP = P G / upe elements per period)
+        const long G = 16 / W;
+        long g = upe, m = G;
+        while (m) { const long r = g % m; g = m; m = r; }
+        const long P = upe / g;
+        if (P * G <= CHUNK_TAB_MAX && (P * G / upe + 1) * t.extent < INT32_MAX / 2) {
+            for (long q = 0; q < P * G; ++q) u.push_back((int)((q / upe) * t.extent + u[(size_t)(q % upe)]));
+            t.tabP[wi] = P;
+        }
+    }
     if (hipMalloc(&t.dunits[wi], u.size() * sizeof(int)) != hipSuccess) {
         t.dunits[wi] = nullptr;
         t.units[wi] = -1;
@@ -629,7 +649,7 @@ static bool unit_table(Type &t, int W, int wi)
         t.units[wi] = -1;
         return false;
     }
-    t.units[wi] = (long)u.size();
+    t.units[wi] = upe;
     return true;
 }
 
@@ -889,16 +909,21 @@ static int launch_merge(Type &t, int wi, const void *src, void *dst, long count,
 // needs only 16-byte tile starts; pack_ept makes them 64-byte ones.)
 #define PACK_TILE 8192               // LDS bytes of extent layout per workgroup
 
-template <int W, int TILE, bool LDSU>
+// TAB: the chunk table (Type::tabP phases after the unit offsets) in LDS
+// instead of the unit offsets: a chunk's G unit offsets are one vector LDS
+// read and one add each, with no per-unit element / unit-index stepping
+template <int W, int TILE, bool LDSU, bool TAB>
 __global__ void __launch_bounds__(256)
 k_pack_tiles(const char *__restrict__ src, char *__restrict__ dst, const int *__restrict__ uoff, long upe, long n,
-             long ext, long lo, long hi, long ept)
+             long ext, long lo, long hi, long ept, long tabP)
 {
     typedef typename UnitT<W>::t V;
     constexpr int G = 16 / W;
     __shared__ pu32x4 s_tile[TILE / 16];
-    __shared__ int s_uoff[LDSU ? MERGE_UNITS_LDS : 1];   // LDSU: as in k_unpack_merge
-    if (LDSU)
+    __shared__ __attribute__((aligned(16))) int s_uoff[LDSU || TAB ? MERGE_UNITS_LDS : 1];   // LDSU: as in k_unpack_merge
+    if (TAB)
+        for (int u = threadIdx.x; u < (int)(tabP * G); u += 256) s_uoff[u] = uoff[upe + u];
+    else if (LDSU)
         for (int u = threadIdx.x; u < (int)upe; u += 256) s_uoff[u] = uoff[u];
     const long i0 = (long)blockIdx.x * ept;
     const long i1 = i0 + ept < n ? i0 + ept : n;
@@ -914,7 +939,33 @@ k_pack_tiles(const char *__restrict__ src, char *__restrict__ dst, const int *__
     // of element i0 + ir sits at ir * ext + e0 + uoff[j] in the tile
     const int up = (int)upe, ext32 = (int)ext;
     const int e0 = (int)(i0 * ext - (long)(a0 - (uintptr_t)src));
+    // TAB: chunk c0 + k P + p is phase p of period k, whose first element is
+    // i0 + k EPP -- the tile starts a period: i0 is a multiple of pack_ept's
+    // step 64 / gcd(size, 64), which EPP = G / gcd(upe, G) divides
+    const unsigned P = (unsigned)tabP;
+    const int epp = TAB ? (int)((long)P * G / upe) : 0;
     for (long c = c0 + threadIdx.x; c < c1; c += 256) {
+        if (TAB && (c + 1) * G <= qn) {
+            const unsigned cr = (unsigned)(c - c0), kk = cr / P, p = cr - kk * P;
+            const int base = (int)kk * epp * ext32 + e0;
+            pu32x4 out = {0, 0, 0, 0};
+#pragma unroll
+            for (int g4 = 0; g4 < G; g4 += 4) {
+                int o[4];
+                if constexpr (G >= 4) {
+                    const pu32x4 t4 = *(const pu32x4 *)&s_uoff[p * G + g4];
+                    o[0] = (int)t4[0]; o[1] = (int)t4[1]; o[2] = (int)t4[2]; o[3] = (int)t4[3];
+                } else {
+#pragma unroll
+                    for (int g = 0; g < G; ++g) o[g] = s_uoff[p * G + g];
+                }
+#pragma unroll
+                for (int g = 0; g < (G < 4 ? G : 4); ++g)
+                    set_unit<W>(out, g4 + g, *(const V *)((const char *)s_tile + base + o[g]));
+            }
+            __builtin_nontemporal_store(out, (pu32x4 *)(dst + 16 * c));
+            continue;
+        }
         const unsigned qr = (unsigned)(c * G - qlo);
         int ir = (int)(qr / (unsigned)up), j = (int)qr - ir * up;
         if ((c + 1) * G <= qn) {
@@ -986,16 +1037,26 @@ static int launch_tiles(Type &t, int wi, const void *src, void *dst, long count,
 {
     const long tiles = (count + ept - 1) / ept;
     if (tiles < 1 || tiles > INT32_MAX) return MPI_ERR_OTHER;
-#define MVX_PACK_TILES_LAUNCH(TL, LU)                                                                            \
-    hipLaunchKernelGGL((k_pack_tiles<W, TL, LU>), dim3((unsigned)tiles), dim3(256), 0, st, (const char *)src,      \
-                       (char *)dst, (const int *)t.dunits[wi], t.units[wi], count, t.extent, lo, hi, ept)
-    const bool lu = t.units[wi] <= MERGE_UNITS_LDS;
+#define MVX_PACK_TILES_LAUNCH(TL, LU, TB)                                                                        \
+    hipLaunchKernelGGL((k_pack_tiles<W, TL, LU, TB>), dim3((unsigned)tiles), dim3(256), 0, st, (const char *)src,  \
+                       (char *)dst, (const int *)t.dunits[wi], t.units[wi], count, t.extent, lo, hi, ept, t.tabP[wi])
+    // MVX_PACK_CHUNK_TAB=0: the unit offsets stepped per unit (A/B)
+    static int tab_on = -1;
+    if (tab_on < 0) {
+        const char *e = getenv("MVX_PACK_CHUNK_TAB");
+        tab_on = e ? atoi(e) != 0 : 1;
+    }
+    // (W = 2 and 1 only: with 2 or 4 units per chunk the table did not pay,
+    // profiles/r06/pack_chunk_tab_ab.txt)
+    const bool tb = tab_on && W <= 2 && t.tabP[wi] > 0, lu = t.units[wi] <= MERGE_UNITS_LDS;
     if (pack_tile_bytes() == 16384) {
-        if (lu) MVX_PACK_TILES_LAUNCH(16384, true);
-        else MVX_PACK_TILES_LAUNCH(16384, false);
+        if (tb) MVX_PACK_TILES_LAUNCH(16384, false, true);
+        else if (lu) MVX_PACK_TILES_LAUNCH(16384, true, false);
+        else MVX_PACK_TILES_LAUNCH(16384, false, false);
     } else {
-        if (lu) MVX_PACK_TILES_LAUNCH(PACK_TILE, true);
-        else MVX_PACK_TILES_LAUNCH(PACK_TILE, false);
+        if (tb) MVX_PACK_TILES_LAUNCH(PACK_TILE, false, true);
+        else if (lu) MVX_PACK_TILES_LAUNCH(PACK_TILE, true, false);
+        else MVX_PACK_TILES_LAUNCH(PACK_TILE, false, false);
     }
 #undef MVX_PACK_TILES_LAUNCH
     return hipGetLastError() == hipSuccess ? MPI_SUCCESS : MPI_ERR_OTHER;
