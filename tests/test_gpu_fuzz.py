@@ -254,3 +254,57 @@ def test_random_op_functions(mvx, oracle, batch):
                 T.assert_same(op, dtype, got, ref)
             except AssertionError as e:
                 raise AssertionError("%s: %s" % (c, e))
+
+
+@pytest.mark.parametrize("batch", range(int(os.environ.get("MVX_FUZZ_REG_BATCHES", "2"))))
+def test_random_op_functions_registered(mvx, oracle, batch):
+    """The op-function sweep with the registration cache on (mode 2: every
+    pageable block is reported with host_invalidate before it is freed), and
+    pageable operand pairs that often share pages: carved from one block,
+    `inoutvec` starting 0-64 bytes after `invec` ends, or before it -- the
+    call-local merge of a call's own operands and the CPU-bounced ranges under
+    another registration (mvx_host.c reg_range) against the oracle's op, with
+    no registration left held after a call."""
+    rng = np.random.default_rng(SEED + 5000 + batch)
+    assert mvx.host_register_enable(True) == 0
+    try:
+        for _ in range(25):
+            c = _op_case(rng)
+            dtype, op, n = c["dtype"], c["op"], c["n"]
+            E = mvx.dtype_info(dtype)[0]
+            n = min(n, (64 << 20) // E)
+            a, b = T.rand_vec(dtype, n, c["seed"]), T.rand_vec(dtype, n, c["seed"] + 1)
+            au8, bu8 = np.ascontiguousarray(a).view(np.uint8), np.ascontiguousarray(b).view(np.uint8)
+            blocks = []
+            if rng.random() < 0.5 and n:
+                # both pageable, from one block: [in][gap][inout] or reversed
+                gap = int(rng.choice([0, E, 16, 64]))
+                nb = au8.nbytes
+                whole = np.zeros(2 * nb + gap + 64, np.uint8)
+                first, second = (0, nb + gap) if rng.random() < 0.5 else (nb + gap, 0)
+                whole[first:first + nb] = au8
+                whole[second:second + nb] = bu8
+                ia, io = whole[first:first + nb], whole[second:second + nb]
+                blocks.append(whole)
+            else:
+                ia, wa = _place(au8, c["kin"], c["sin"], E)
+                io, wio = _place(bu8, c["kio"], c["sio"], E)
+                blocks += [w for w in (wa, wio) if isinstance(w, np.ndarray)]
+            ref = T.clone(b)
+            rc_ref = oracle.op(op, dtype, au8, ref.view(np.uint8), n)
+            mvx.op_errno()
+            mvx.MPIR_call(MPIR_NAMES[op], ia, io, n, dtype)
+            rc = mvx.op_errno()
+            assert rc == rc_ref, (rc, rc_ref, c)
+            got = _back(io)[: n * E]
+            if n:
+                try:
+                    T.assert_same(op, dtype, got, ref)
+                except AssertionError as e:
+                    raise AssertionError("%s: %s" % (c, e))
+            assert mvx.host_register_deferred()["held"] == 0, c
+            for w in blocks:                          # mode 2: report before the free
+                mvx.host_invalidate(w.ctypes.data, w.nbytes)
+            del blocks
+    finally:
+        mvx.host_register_enable(False)
