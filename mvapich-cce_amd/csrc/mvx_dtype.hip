@@ -60,6 +60,9 @@ struct Type {
     // units of a 16-byte packed chunk, per chunk phase -- tabP[w] phases
     // (a period of tabP chunks holds whole elements), 0: no table
     long tabP[5];
+    // the tile kernels' LDS swizzle for W (swz_pick): 0 none, else s -- bits
+    // [s, s + 3) of a tile byte address XORed into its 16-byte slot index
+    int swz[5];
     // whole-word unpack (merge_ok): 0 not decided, 1 yes, -1 no; the map's
     // reach [mlo, mhi) around the element origin
     int merge;
@@ -609,6 +612,52 @@ k_pack_units(const char *__restrict__ src, char *__restrict__ dst, const int *__
     }
 }
 
+// LDS bank conflicts of the tile kernels' unit accesses, modelled
+// (MI355X_MICROARCH.md LDS: 1-, 2- and 4-byte reads and every write bank
+// (a / 4) mod 32 over 32-lane groups, 8-byte reads mod 64): lane l of a group
+// takes chunk l, units G l .. G l + G - 1 of the stream, so when an element's
+// units repeat every 128 or 256 bytes of the extent layout, lanes a few
+// apart hit one bank (struct {char; hole; int}: 7-way, every other float:
+// 8-way).  Swizzle candidates s = 7, 8, 9 (tile byte a lives at
+// a ^ (((a >> s) & 7) << 4): 16-byte slots permuted within 128-byte rows,
+// so whole 16-byte words stay whole) against none, averaged over a few
+// group starts and element offsets in the tile; the best if it saves a
+// fifth of the extra cycles, else 0.
+static int swz_pick(const std::vector<int> &u, long upe, long ext, int W)
+{
+    const int G = 16 / W, banks = W == 8 ? 64 : 32;
+    const int cand[4] = {0, 7, 8, 9};
+    const long starts[4] = {0, 13, 32, 77}, offs[3] = {0, 5, 10};
+    double cost[4] = {0, 0, 0, 0};
+    if (ext <= 0 || ext > 4096 || upe <= 0) return 0;
+    for (int ci = 0; ci < 4; ++ci)
+        for (long st : starts)
+            for (long e0 : offs)
+                for (int g = 0; g < G; ++g) {
+                    long dw[32];
+                    int n = 0, worst = 1;
+                    for (int l = 0; l < 32; ++l) {
+                        const long q = (st + l) * G + g, e = q / upe, j = q % upe;
+                        long a = e * ext + e0 + u[(size_t)j] + 64;      // (+64: offsets may be negative)
+                        if (cand[ci]) a ^= ((a >> cand[ci]) & 7) << 4;
+                        const long d = a / 4;
+                        bool dup = false;
+                        for (int k = 0; k < n && !dup; ++k) dup = dw[k] == d;
+                        if (!dup) dw[n++] = d;
+                    }
+                    for (int k = 0; k < n; ++k) {
+                        int same = 0;
+                        for (int m = 0; m < n; ++m) same += dw[m] % banks == dw[k] % banks;
+                        if (same > worst) worst = same;
+                    }
+                    cost[ci] += worst - 1;
+                }
+    int best = 0;
+    for (int ci = 1; ci < 4; ++ci)
+        if (cost[ci] < cost[best]) best = ci;
+    return best && cost[best] <= 0.8 * cost[0] ? cand[best] : 0;
+}
+
 // the unit table for W (index wi), built once per type; false if the map
 // does not split into W-byte units
 static bool unit_table(Type &t, int W, int wi)
@@ -638,6 +687,7 @@ static bool unit_table(Type &t, int W, int wi)
             t.tabP[wi] = P;
         }
     }
+    t.swz[wi] = W <= 8 ? swz_pick(u, upe, t.extent, W) : 0;
     if (hipMalloc(&t.dunits[wi], u.size() * sizeof(int)) != hipSuccess) {
         t.dunits[wi] = nullptr;
         t.units[wi] = -1;
@@ -707,6 +757,9 @@ template <> __device__ inline uint8_t unit_of<1>(const pu32x4 &v, int g)
     return (uint8_t)(v[g >> 2] >> (8 * (g & 3)));
 }
 
+// the LDS byte address of tile byte a under the swizzle (Type::swz)
+template <bool SWZ> __device__ inline int lds_at(int a, int s) { return SWZ ? a ^ (((a >> s) & 7) << 4) : a; }
+
 // unit g (W bytes) of a 16-byte chunk being assembled
 template <int W> __device__ inline void set_unit(pu32x4 &v, int g, typename UnitT<W>::t x);
 template <> __device__ inline void set_unit<8>(pu32x4 &v, int g, pu32x2 x)
@@ -734,10 +787,10 @@ template <> __device__ inline void set_unit<1>(pu32x4 &v, int g, uint8_t x)
 // trash word past its end (a select on the LDS address, no branch), and the
 // hull's two edge words are stored byte by byte, so every unit of the tile
 // is one LDS store.
-template <int W, int TILE, bool LDSU>
+template <int W, int TILE, bool LDSU, bool SWZ>
 __global__ void __launch_bounds__(256)
 k_unpack_merge(const char *__restrict__ packed, char *__restrict__ dst, const int *__restrict__ uoff, long upe,
-               long n, long ext, long lo, long hi, uintptr_t a0, uintptr_t h0, uintptr_t h1)
+               long n, long ext, long lo, long hi, uintptr_t a0, uintptr_t h0, uintptr_t h1, int swz)
 {
     typedef typename UnitT<W>::t V;
     __shared__ pu32x4 s_tile[TILE / 16 + 1];            // + the trash word
@@ -749,7 +802,8 @@ k_unpack_merge(const char *__restrict__ packed, char *__restrict__ dst, const in
                                                                            : ((h1 + 15) & ~(uintptr_t)15);
     const int nw = (int)((tend - t0) / 16);
     for (int w = threadIdx.x; w < nw; w += 256)
-        s_tile[w] = __builtin_nontemporal_load((const pu32x4 *)(t0 + 16 * (uintptr_t)w));
+        *(pu32x4 *)((char *)s_tile + lds_at<SWZ>(16 * w, swz)) =
+            __builtin_nontemporal_load((const pu32x4 *)(t0 + 16 * (uintptr_t)w));
     __syncthreads();
     // the elements whose maps reach into [t0, tend): relative to dst
     const long a = (long)(t0 - (uintptr_t)dst), b = (long)(tend - (uintptr_t)dst);
@@ -797,7 +851,7 @@ k_unpack_merge(const char *__restrict__ packed, char *__restrict__ dst, const in
 #pragma unroll
             for (int g = 0; g < G; ++g) {
                 const bool in = (g < valid) & ((unsigned)rel[g] < (unsigned)span);
-                *(V *)((char *)s_tile + (in ? rel[g] : TILE)) = unit_of<W>(v[u], g);
+                *(V *)((char *)s_tile + (in ? lds_at<SWZ>(rel[g], swz) : TILE)) = unit_of<W>(v[u], g);
             }
         }
     }
@@ -805,12 +859,26 @@ k_unpack_merge(const char *__restrict__ packed, char *__restrict__ dst, const in
     for (int w = threadIdx.x; w < nw; w += 256) {
         const uintptr_t at = t0 + 16 * (uintptr_t)w;
         if (at >= h0 && at + 16 <= h1) {
-            __builtin_nontemporal_store(s_tile[w], (pu32x4 *)at);
+            __builtin_nontemporal_store(*(const pu32x4 *)((const char *)s_tile + lds_at<SWZ>(16 * w, swz)),
+                                        (pu32x4 *)at);
         } else {                                   // an edge word of the hull: its hull bytes only
             const uintptr_t b0 = at > h0 ? at : h0, b1 = at + 16 < h1 ? at + 16 : h1;
-            for (uintptr_t b = b0; b < b1; ++b) *(char *)b = ((const char *)s_tile)[16 * w + (b - at)];
+            const char *word = (const char *)s_tile + lds_at<SWZ>(16 * w, swz);
+            for (uintptr_t b = b0; b < b1; ++b) *(char *)b = word[b - at];
         }
     }
+}
+
+// MVX_LDS_SWIZZLE=0: the tile kernels keep their LDS layout linear (A/B;
+// Type::swz, swz_pick)
+static int swz_on()
+{
+    static int on = -1;
+    if (on < 0) {
+        const char *e = getenv("MVX_LDS_SWIZZLE");
+        on = e ? atoi(e) != 0 : 1;
+    }
+    return on;
 }
 
 // MVX_UNPACK_MERGE: 1 (default) unpack by whole words where the type's map
@@ -869,29 +937,23 @@ static int launch_merge(Type &t, int wi, const void *src, void *dst, long count,
     const long upe = t.units[wi];
     const uintptr_t h0 = (uintptr_t)dst + lo, h1 = (uintptr_t)dst + (count - 1) * t.extent + hi;
     const uintptr_t a0 = h0 & ~(uintptr_t)15;
-    // MVX_UNPACK_TILE_KIB: 8 (default) or 16 (tuning; 4 KiB ran 30-40 %
-    // slower, 16 within a few per cent either way, profiles/r06/pack_tile_sizes.txt)
-    static long TILE = 0;
-    if (!TILE) {
-        const char *e = getenv("MVX_UNPACK_TILE_KIB");
-        TILE = e && atoi(e) == 16 ? 16384 : MERGE_TILE;
-    }
-    // (the 16 KiB tuning tile only with the unit offsets in LDS)
-    const long T = upe > MERGE_UNITS_LDS ? MERGE_TILE : TILE;
-    const long tiles = (long)((((h1 + 15) & ~(uintptr_t)15) - a0 + T - 1) / T);
+    // 8 KiB tiles (4 KiB ran 30-40 % slower, 16 KiB 0-8 % slower:
+    // profiles/r06/pack_tile_sizes.txt, pack_tile_sizes_noflat.txt)
+    const long tiles = (long)((((h1 + 15) & ~(uintptr_t)15) - a0 + MERGE_TILE - 1) / MERGE_TILE);
     if (tiles < 1 || tiles > INT32_MAX) return MPI_ERR_OTHER;
-    if (upe > MERGE_UNITS_LDS)
-        hipLaunchKernelGGL((k_unpack_merge<W, MERGE_TILE, false>), dim3((unsigned)tiles), dim3(256), 0, st,
-                           (const char *)src, (char *)dst, (const int *)t.dunits[wi], upe, count, t.extent, lo, hi,
-                           a0, h0, h1);
-    else if (TILE == 16384)
-        hipLaunchKernelGGL((k_unpack_merge<W, 16384, true>), dim3((unsigned)tiles), dim3(256), 0, st,
-                           (const char *)src, (char *)dst, (const int *)t.dunits[wi], upe, count, t.extent, lo, hi,
-                           a0, h0, h1);
-    else
-        hipLaunchKernelGGL((k_unpack_merge<W, MERGE_TILE, true>), dim3((unsigned)tiles), dim3(256), 0, st,
-                           (const char *)src, (char *)dst, (const int *)t.dunits[wi], upe, count, t.extent, lo, hi,
-                           a0, h0, h1);
+    const int sw = swz_on() ? t.swz[wi] : 0;
+#define MVX_MERGE_LAUNCH(LU, SW)                                                                                   \
+    hipLaunchKernelGGL((k_unpack_merge<W, MERGE_TILE, LU, SW>), dim3((unsigned)tiles), dim3(256), 0, st,           \
+                       (const char *)src, (char *)dst, (const int *)t.dunits[wi], upe, count, t.extent, lo, hi, a0, \
+                       h0, h1, sw)
+    if (upe > MERGE_UNITS_LDS) {
+        if (sw) MVX_MERGE_LAUNCH(false, true);
+        else MVX_MERGE_LAUNCH(false, false);
+    } else {
+        if (sw) MVX_MERGE_LAUNCH(true, true);
+        else MVX_MERGE_LAUNCH(true, false);
+    }
+#undef MVX_MERGE_LAUNCH
     return hipGetLastError() == hipSuccess ? MPI_SUCCESS : MPI_ERR_OTHER;
 }
 
@@ -912,10 +974,10 @@ static int launch_merge(Type &t, int wi, const void *src, void *dst, long count,
 // TAB: the chunk table (Type::tabP phases after the unit offsets) in LDS
 // instead of the unit offsets: a chunk's G unit offsets are one vector LDS
 // read and one add each, with no per-unit element / unit-index stepping
-template <int W, int TILE, bool LDSU, bool TAB>
+template <int W, int TILE, bool LDSU, bool TAB, bool SWZ>
 __global__ void __launch_bounds__(256)
 k_pack_tiles(const char *__restrict__ src, char *__restrict__ dst, const int *__restrict__ uoff, long upe, long n,
-             long ext, long lo, long hi, long ept, long tabP)
+             long ext, long lo, long hi, long ept, long tabP, int swz)
 {
     typedef typename UnitT<W>::t V;
     constexpr int G = 16 / W;
@@ -931,7 +993,8 @@ k_pack_tiles(const char *__restrict__ src, char *__restrict__ dst, const int *__
     const uintptr_t a1 = ((uintptr_t)src + (i1 - 1) * ext + hi + 15) & ~(uintptr_t)15;
     const int nw = (int)((a1 - a0) / 16);
     for (int w = threadIdx.x; w < nw; w += 256)
-        s_tile[w] = __builtin_nontemporal_load((const pu32x4 *)(a0 + 16 * (uintptr_t)w));
+        *(pu32x4 *)((char *)s_tile + lds_at<SWZ>(16 * w, swz)) =
+            __builtin_nontemporal_load((const pu32x4 *)(a0 + 16 * (uintptr_t)w));
     __syncthreads();
     const long qn = n * upe, qlo = i0 * upe, qhi = i1 * upe;
     const long c0 = qlo / G, c1 = (qhi + G - 1) / G;      // qlo is a multiple of G (ept)
@@ -961,7 +1024,7 @@ k_pack_tiles(const char *__restrict__ src, char *__restrict__ dst, const int *__
                 }
 #pragma unroll
                 for (int g = 0; g < (G < 4 ? G : 4); ++g)
-                    set_unit<W>(out, g4 + g, *(const V *)((const char *)s_tile + base + o[g]));
+                    set_unit<W>(out, g4 + g, *(const V *)((const char *)s_tile + lds_at<SWZ>(base + o[g], swz)));
             }
             __builtin_nontemporal_store(out, (pu32x4 *)(dst + 16 * c));
             continue;
@@ -973,14 +1036,14 @@ k_pack_tiles(const char *__restrict__ src, char *__restrict__ dst, const int *__
 #pragma unroll
             for (int g = 0; g < G; ++g) {
                 const int rel = ir * ext32 + e0 + (LDSU ? s_uoff[j] : uoff[j]);
-                set_unit<W>(out, g, *(const V *)((const char *)s_tile + rel));
+                set_unit<W>(out, g, *(const V *)((const char *)s_tile + lds_at<SWZ>(rel, swz)));
                 if (++j == up) { j = 0; ++ir; }
             }
             __builtin_nontemporal_store(out, (pu32x4 *)(dst + 16 * c));
         } else {
             for (long q = c * G; q < qn; ++q) {
                 const int rel = ir * ext32 + e0 + (LDSU ? s_uoff[j] : uoff[j]);
-                *(V *)(dst + q * W) = *(const V *)((const char *)s_tile + rel);
+                *(V *)(dst + q * W) = *(const V *)((const char *)s_tile + lds_at<SWZ>(rel, swz));
                 if (++j == up) { j = 0; ++ir; }
             }
         }
@@ -999,27 +1062,15 @@ static int tiles_on()
     return on;
 }
 
-// MVX_PACK_TILE_KIB: the tile (LDS) size, 8 (default) or 16 (tuning).  8
-// KiB tiles leave room for 8 resident workgroups per CU; 16 KiB (6 per CU,
-// LDS-bound) and 4 KiB (too little work per tile) ran slower
-// (profiles/r06/pack_tile_sizes.txt: struct {int; hole; double} 80.2 / 85.1 /
-// 92.9 us for 8 / 16 / 4 KiB against 91.4 for the unit kernel).
-static int pack_tile_bytes()
-{
-    static int b = 0;
-    if (!b) {
-        const char *e = getenv("MVX_PACK_TILE_KIB");
-        b = e && atoi(e) == 16 ? 16384 : PACK_TILE;
-    }
-    return b;
-}
-
 // elements per tile (a multiple of 64 / gcd(size, 64): each tile's packed
 // bytes start on a 64-byte sector, so no two workgroups write one sector;
 // its hull within the tile with the alignment slack), or 0: no tiling
 static long pack_ept(const Type &t, long lo, long hi)
 {
-    const long TILE = pack_tile_bytes();
+    // 8 KiB tiles leave room for 8 resident workgroups per CU; 16 KiB (6 per
+    // CU, LDS-bound) and 4 KiB (too little work per tile) ran slower
+    // (profiles/r06/pack_tile_sizes.txt, pack_tile_sizes_noflat.txt)
+    const long TILE = PACK_TILE;
     if (t.extent <= 0 || t.extent > (1L << 30) || t.size <= 0 || hi - lo > TILE / 4) return 0;
     long g = t.size, m = 64;
     while (m) { const long r = g % m; g = m; m = r; }
@@ -1037,9 +1088,10 @@ static int launch_tiles(Type &t, int wi, const void *src, void *dst, long count,
 {
     const long tiles = (count + ept - 1) / ept;
     if (tiles < 1 || tiles > INT32_MAX) return MPI_ERR_OTHER;
-#define MVX_PACK_TILES_LAUNCH(TL, LU, TB)                                                                        \
-    hipLaunchKernelGGL((k_pack_tiles<W, TL, LU, TB>), dim3((unsigned)tiles), dim3(256), 0, st, (const char *)src,  \
-                       (char *)dst, (const int *)t.dunits[wi], t.units[wi], count, t.extent, lo, hi, ept, t.tabP[wi])
+#define MVX_PACK_TILES_LAUNCH(LU, TB, SW)                                                                        \
+    hipLaunchKernelGGL((k_pack_tiles<W, PACK_TILE, LU, TB, SW>), dim3((unsigned)tiles), dim3(256), 0, st,          \
+                       (const char *)src, (char *)dst, (const int *)t.dunits[wi], t.units[wi], count, t.extent, lo,  \
+                       hi, ept, t.tabP[wi], sw)
     // MVX_PACK_CHUNK_TAB=0: the unit offsets stepped per unit (A/B)
     static int tab_on = -1;
     if (tab_on < 0) {
@@ -1049,14 +1101,20 @@ static int launch_tiles(Type &t, int wi, const void *src, void *dst, long count,
     // (W = 2 and 1 only: with 2 or 4 units per chunk the table did not pay,
     // profiles/r06/pack_chunk_tab_ab.txt)
     const bool tb = tab_on && W <= 2 && t.tabP[wi] > 0, lu = t.units[wi] <= MERGE_UNITS_LDS;
-    if (pack_tile_bytes() == 16384) {
-        if (tb) MVX_PACK_TILES_LAUNCH(16384, false, true);
-        else if (lu) MVX_PACK_TILES_LAUNCH(16384, true, false);
-        else MVX_PACK_TILES_LAUNCH(16384, false, false);
+    // the swizzle for 1- and 2-byte units only: G = 16 / W LDS reads per
+    // chunk; at W = 4 it cost its address arithmetic and gained nothing
+    // (struct {int; hole; double} 74.5-75.1 -> 75.6-75.9 us, whose unpack it
+    // takes 114.8 -> 113.9; profiles/r06/lds_swizzle_ab.txt)
+    const int sw = swz_on() && W <= 2 ? t.swz[wi] : 0;
+    if (tb) {
+        if (sw) MVX_PACK_TILES_LAUNCH(false, true, true);
+        else MVX_PACK_TILES_LAUNCH(false, true, false);
+    } else if (lu) {
+        if (sw) MVX_PACK_TILES_LAUNCH(true, false, true);
+        else MVX_PACK_TILES_LAUNCH(true, false, false);
     } else {
-        if (tb) MVX_PACK_TILES_LAUNCH(PACK_TILE, false, true);
-        else if (lu) MVX_PACK_TILES_LAUNCH(PACK_TILE, true, false);
-        else MVX_PACK_TILES_LAUNCH(PACK_TILE, false, false);
+        if (sw) MVX_PACK_TILES_LAUNCH(false, false, true);
+        else MVX_PACK_TILES_LAUNCH(false, false, false);
     }
 #undef MVX_PACK_TILES_LAUNCH
     return hipGetLastError() == hipSuccess ? MPI_SUCCESS : MPI_ERR_OTHER;

@@ -76,9 +76,13 @@ def test_repeat_calls_hit_the_cache(mvx, mib):
         _sum_call(mvx, a, y, n)
         assert np.array_equal(y, want), rep
     s1 = mvx.host_register_stats()
-    assert s1["entries"] >= 2 and s1["misses"] - s0["misses"] == 2, (s0, s1)
+    # both operands registered: an entry each, or one union when their
+    # allocations share a page (the call's own operands merge)
+    assert s1["misses"] - s0["misses"] == 2, (s0, s1)
+    assert s1["entries"] - s0["entries"] >= 1 and s1["bytes"] - s0["bytes"] >= 2 * n * 4, (s0, s1)
     assert s1["hits"] - s0["hits"] >= 4, (s0, s1)
-    assert mvx.host_unregister(a) == 0 and mvx.host_unregister(y) == 0
+    assert mvx.host_unregister(a) == 0
+    mvx.host_unregister(y)                      # its own entry, or gone with a's union
     assert mvx.host_unregister(a) != 0          # nothing left at that address
 
 
