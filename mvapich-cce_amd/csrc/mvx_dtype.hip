@@ -28,6 +28,7 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <algorithm>
 #include <vector>
 
 #include "mvx_mpi.h"
@@ -635,21 +636,19 @@ static int swz_pick(const std::vector<int> &u, long upe, long ext, int W)
             for (long e0 : offs)
                 for (int g = 0; g < G; ++g) {
                     long dw[32];
-                    int n = 0, worst = 1;
+                    int per[64] = {0}, worst = 1;
                     for (int l = 0; l < 32; ++l) {
                         const long q = (st + l) * G + g, e = q / upe, j = q % upe;
-                        long a = e * ext + e0 + u[(size_t)j] + 64;      // (+64: offsets may be negative)
+                        long a = e * ext + e0 + u[(size_t)j] + 4096;    // (offsets may be negative)
                         if (cand[ci]) a ^= ((a >> cand[ci]) & 7) << 4;
-                        const long d = a / 4;
-                        bool dup = false;
-                        for (int k = 0; k < n && !dup; ++k) dup = dw[k] == d;
-                        if (!dup) dw[n++] = d;
+                        dw[l] = a / 4;
                     }
-                    for (int k = 0; k < n; ++k) {
-                        int same = 0;
-                        for (int m = 0; m < n; ++m) same += dw[m] % banks == dw[k] % banks;
-                        if (same > worst) worst = same;
-                    }
+                    std::sort(dw, dw + 32);                        // distinct dwords per bank
+                    for (int l = 0; l < 32; ++l)
+                        if (!l || dw[l] != dw[l - 1]) {
+                            const int c = ++per[dw[l] % banks];
+                            if (c > worst) worst = c;
+                        }
                     cost[ci] += worst - 1;
                 }
     int best = 0;
