@@ -458,3 +458,43 @@ def test_random_type_maps_pack_unpack(mvx, oracle, batch):
             for m in reversed(made):
                 mvx.MPI_Type_free(m)
                 oracle.type_free(m)
+
+
+def test_whole_word_unpack_of_large_elements(mvx, oracle):
+    """Whole-word unpack of types with more than 2048 units per element (the
+    unit offsets then come from global memory, k_unpack_merge<..., LDSU =
+    false, ...>): 2 chars of every 3, 1100 and 1400 blocks (extents 3299 and
+    4199 bytes; the first within the LDS-swizzle model's reach), against the
+    oracle's type-map copy with guard bands, at several counts and origin
+    phases."""
+    import torch
+    made = [
+        _both(mvx, oracle, "hindexed", 1100, [2] * 1100, [3 * i for i in range(1100)], C),
+        _both(mvx, oracle, "hindexed", 1400, [2] * 1400, [3 * i for i in range(1400)], C),
+    ]
+    try:
+        for h in made:
+            ext = mvx.MPI_Type_extent(h)[1]
+            size = mvx.MPI_Type_size(h)[1]
+            L = mvx.type_layout(h)
+            for n in (1, 2, 3, 100, 3001):
+                for phase in (0, 7):
+                    guard = 256
+                    off = guard + phase
+                    nb = off + (n - 1) * ext + L["span_hi"] + guard
+                    rng = np.random.default_rng(n * 11 + phase + h)
+                    x = rng.integers(0, 256, nb, dtype=np.uint8)
+                    y0 = rng.integers(0, 256, nb, dtype=np.uint8)
+                    dx = torch.from_numpy(x).cuda()
+                    dy = torch.from_numpy(y0).cuda()
+                    dp = torch.zeros(max(n * size, 16), dtype=torch.uint8, device="cuda")
+                    assert mvx.type_pack(h, dx.data_ptr() + off, dp, n) == 0
+                    assert mvx.type_unpack(h, dp, dy.data_ptr() + off, n) == 0
+                    ref = y0.copy()
+                    assert oracle.type_copy(ref[off:], x[off:], n, h) == 0
+                    got = T.from_dev(dy)
+                    assert np.array_equal(got, ref), (ext, n, phase, np.flatnonzero(got != ref)[:8])
+    finally:
+        for h in made:
+            mvx.MPI_Type_free(h)
+            oracle.type_free(h)
