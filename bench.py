@@ -198,6 +198,27 @@ def worker_env(base, rank, n, port):
     return env
 
 
+class _StdoutToStderr:
+    """fd 1 points at stderr while native code that reports on stdout runs
+    (gloo prints each rank's connection count when the process group
+    forms): the driver reads rank 0's one JSON line from stdout, and under
+    torchrun every rank's stdout is merged into it."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+        return self
+
+    def __exit__(self, *exc):
+        import ctypes
+        sys.stdout.flush()
+        ctypes.CDLL(None).fflush(None)       # C stdio's buffer, before fd 1 goes back
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+        return False
+
+
 def _rc_of(rc):
     return 128 - rc if rc < 0 else rc      # a signal -> 128 + signo, as a shell reports it
 
@@ -307,18 +328,18 @@ def launch(args, n, argv):
     reader.join(timeout=10)
     rcs = [p.returncode for p in procs]
     wall = time.time() - t0
-    for line in out0:
+    for line in out0:                  # stdout carries the JSON line only; the rest goes to stderr
         if line.startswith("{"):
             try:
                 d = json.loads(line)
             except ValueError:
-                print(line, flush=True)
+                print(line, file=sys.stderr, flush=True)
                 continue
             d["launch"] = {"mode": "self (bench.py --gpus %d without a launcher: %d worker processes)" % (n, n),
                            "workers": n, "wall_s": round(wall, 3), "worker_rcs": rcs}
             print(json.dumps(d), flush=True)
         else:
-            print(line, flush=True)
+            print(line, file=sys.stderr, flush=True)
     return max(_rc_of(rc) for rc in rcs)
 
 
@@ -1393,8 +1414,10 @@ def main(argv=None):
     # instead of gloo's 30 minutes; rank 0's reference run (tens of seconds
     # at C5 x 8) stays well inside it
     import datetime
-    dist.init_process_group("gloo", rank=rank, world_size=world,
-                            timeout=datetime.timedelta(seconds=args.gloo_timeout))
+    with _StdoutToStderr():
+        dist.init_process_group("gloo", rank=rank, world_size=world,
+                                timeout=datetime.timedelta(seconds=args.gloo_timeout))
+        dist.barrier()                       # (the connections form here or above)
     clock.mark("start-up (imports, process group)")
     out, emit = run_multi(args, mvx, dev, world, rank, local, clock)
     emit(out)

@@ -203,3 +203,38 @@ def test_mix_ceiling_summary():
     assert abs(d["mixed_line_GBs"] - (read + (copy - read) * 2 / 3)) < 0.1
     assert d["frac_of_additive"] == round(6400.0 / (3 * nb / 120e-6 / 1e9), 4)
     assert copy < d["mixed_line_GBs"] < read
+
+
+_CHATTER = r'''
+import datetime, os, sys
+sys.path.insert(0, sys.argv[1])
+import torch.distributed as dist
+import bench
+rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+with bench._StdoutToStderr():
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=60))
+    dist.barrier()
+if rank == 0:
+    print('{"metric": "x"}')
+dist.destroy_process_group()
+'''
+
+
+def test_gloo_connection_report_stays_off_stdout(tmp_path):
+    """gloo prints each rank's connection count on stdout when the process
+    group forms; under torchrun every rank's stdout is the driver's, which
+    reads rank 0's one JSON line there.  bench.py forms the group inside
+    _StdoutToStderr: stdout is the JSON line alone."""
+    import socket
+    import subprocess
+    script = tmp_path / "chatter.py"
+    script.write_text(_CHATTER)
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "3",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), str(script), repo],
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout.strip().splitlines() == ['{"metric": "x"}'], r.stdout
