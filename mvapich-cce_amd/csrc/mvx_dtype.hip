@@ -786,15 +786,17 @@ template <> __device__ inline void set_unit<1>(pu32x4 &v, int g, uint8_t x)
 // trash word past its end (a select on the LDS address, no branch), and the
 // hull's two edge words are stored byte by byte, so every unit of the tile
 // is one LDS store.
-template <int W, int TILE, bool LDSU, bool SWZ>
+template <int W, int TILE, bool LDSU, bool SWZ, bool TAB>
 __global__ void __launch_bounds__(256)
 k_unpack_merge(const char *__restrict__ packed, char *__restrict__ dst, const int *__restrict__ uoff, long upe,
-               long n, long ext, long lo, long hi, uintptr_t a0, uintptr_t h0, uintptr_t h1, int swz)
+               long n, long ext, long lo, long hi, uintptr_t a0, uintptr_t h0, uintptr_t h1, int swz, long tabP)
 {
     typedef typename UnitT<W>::t V;
     __shared__ pu32x4 s_tile[TILE / 16 + 1];            // + the trash word
-    __shared__ int s_uoff[LDSU ? MERGE_UNITS_LDS : 1];
-    if (LDSU)
+    __shared__ __attribute__((aligned(16))) int s_uoff[LDSU || TAB ? MERGE_UNITS_LDS : 1];
+    if (TAB)                                            // the chunk table (k_pack_tiles)
+        for (int u = threadIdx.x; u < (int)(tabP * (16 / W)); u += 256) s_uoff[u] = uoff[upe + u];
+    else if (LDSU)
         for (int u = threadIdx.x; u < (int)upe; u += 256) s_uoff[u] = uoff[u];
     const uintptr_t t0 = a0 + (uintptr_t)blockIdx.x * TILE;                // this tile's first word
     const uintptr_t tend = t0 + TILE < ((h1 + 15) & ~(uintptr_t)15) ? t0 + TILE
@@ -818,6 +820,11 @@ k_unpack_merge(const char *__restrict__ packed, char *__restrict__ dst, const in
     const int up = (int)upe, ext32 = (int)ext, span = (int)(tend - t0);
     const int e0 = (int)(ilo * ext - a);
     const long q0 = ilo * upe, qn = n * upe, c0 = q0 / G, c1 = (ihi * upe + G - 1) / G;
+    // TAB: chunk c0 + d is phase (p0 + d) % P of period k0 + (p0 + d) / P,
+    // whose first element is (k0 + ...) EPP; relative to element ilo: b0
+    const unsigned P = (unsigned)tabP, p0 = TAB ? (unsigned)(c0 % (long)P) : 0;
+    const int epp = TAB ? (int)((long)P * G / upe) : 0;
+    const int b0 = TAB ? (int)(c0 / (long)P * epp - ilo) : 0;
     for (long c = c0 + threadIdx.x; c < c1; c += 512) {
         pu32x4 v[2];
 #pragma unroll
@@ -834,18 +841,35 @@ k_unpack_merge(const char *__restrict__ packed, char *__restrict__ dst, const in
                 v[u] = pu32x4{0, 0, 0, 0};
                 for (int g = 0; g < valid; ++g) set_unit<W>(v[u], g, *(const V *)(packed + (cc * G + g) * W));
             }
-            // > -G: the first chunk may start in elements before ilo (several
-            // when an element has fewer than G units), whose units all land
-            // below the tile (ilo is the first element reaching it); ir is
-            // the floor of qr / up, so j is a unit index in every case
-            const int qr = (int)(cc * G - q0);
-            int ir = qr >= 0 ? (int)((unsigned)qr / (unsigned)up) : -(int)((unsigned)(up - 1 - qr) / (unsigned)up);
-            int j = qr - ir * up;
             int rel[G];
+            if constexpr (TAB) {
+                const unsigned cr = (unsigned)(cc - c0) + p0, kk = cr / P, p = cr - kk * P;
+                const int base = (b0 + (int)kk * epp) * ext32 + e0;
 #pragma unroll
-            for (int g = 0; g < G; ++g) {
-                rel[g] = ir * ext32 + e0 + (LDSU ? s_uoff[j] : uoff[j]);
-                if (++j == up) { j = 0; ++ir; }
+                for (int g4 = 0; g4 < G; g4 += 4) {
+                    if constexpr (G >= 4) {
+                        const pu32x4 t4 = *(const pu32x4 *)&s_uoff[p * G + g4];
+#pragma unroll
+                        for (int g = 0; g < 4; ++g) rel[g4 + g] = base + (int)t4[g];
+                    } else {
+#pragma unroll
+                        for (int g = 0; g < G; ++g) rel[g] = base + s_uoff[p * G + g];
+                    }
+                }
+            } else {
+                // > -G: the first chunk may start in elements before ilo
+                // (several when an element has fewer than G units), whose
+                // units all land below the tile (ilo is the first element
+                // reaching it); ir is the floor of qr / up, so j is a unit
+                // index in every case
+                const int qr = (int)(cc * G - q0);
+                int ir = qr >= 0 ? (int)((unsigned)qr / (unsigned)up) : -(int)((unsigned)(up - 1 - qr) / (unsigned)up);
+                int j = qr - ir * up;
+#pragma unroll
+                for (int g = 0; g < G; ++g) {
+                    rel[g] = ir * ext32 + e0 + (LDSU ? s_uoff[j] : uoff[j]);
+                    if (++j == up) { j = 0; ++ir; }
+                }
             }
 #pragma unroll
             for (int g = 0; g < G; ++g) {
@@ -866,6 +890,18 @@ k_unpack_merge(const char *__restrict__ packed, char *__restrict__ dst, const in
             for (uintptr_t b = b0; b < b1; ++b) *(char *)b = word[b - at];
         }
     }
+}
+
+// MVX_UNPACK_CHUNK_TAB=0: the whole-word unpack steps its unit offsets per
+// unit (A/B)
+static int merge_tab_on()
+{
+    static int on = -1;
+    if (on < 0) {
+        const char *e = getenv("MVX_UNPACK_CHUNK_TAB");
+        on = e ? atoi(e) != 0 : 1;
+    }
+    return on;
 }
 
 // MVX_LDS_SWIZZLE=0: the tile kernels keep their LDS layout linear (A/B;
@@ -941,16 +977,21 @@ static int launch_merge(Type &t, int wi, const void *src, void *dst, long count,
     const long tiles = (long)((((h1 + 15) & ~(uintptr_t)15) - a0 + MERGE_TILE - 1) / MERGE_TILE);
     if (tiles < 1 || tiles > INT32_MAX) return MPI_ERR_OTHER;
     const int sw = swz_on() ? t.swz[wi] : 0;
-#define MVX_MERGE_LAUNCH(LU, SW)                                                                                   \
-    hipLaunchKernelGGL((k_unpack_merge<W, MERGE_TILE, LU, SW>), dim3((unsigned)tiles), dim3(256), 0, st,           \
+#define MVX_MERGE_LAUNCH(LU, SW, TB)                                                                               \
+    hipLaunchKernelGGL((k_unpack_merge<W, MERGE_TILE, LU, SW, TB>), dim3((unsigned)tiles), dim3(256), 0, st,       \
                        (const char *)src, (char *)dst, (const int *)t.dunits[wi], upe, count, t.extent, lo, hi, a0, \
-                       h0, h1, sw)
-    if (upe > MERGE_UNITS_LDS) {
-        if (sw) MVX_MERGE_LAUNCH(false, true);
-        else MVX_MERGE_LAUNCH(false, false);
+                       h0, h1, sw, t.tabP[wi])
+    // the chunk table for 1- and 2-byte units (as k_pack_tiles; MVX_PACK_CHUNK_TAB)
+    const bool tb = merge_tab_on() && W <= 2 && t.tabP[wi] > 0;
+    if (tb) {
+        if (sw) MVX_MERGE_LAUNCH(false, true, true);
+        else MVX_MERGE_LAUNCH(false, false, true);
+    } else if (upe > MERGE_UNITS_LDS) {
+        if (sw) MVX_MERGE_LAUNCH(false, true, false);
+        else MVX_MERGE_LAUNCH(false, false, false);
     } else {
-        if (sw) MVX_MERGE_LAUNCH(true, true);
-        else MVX_MERGE_LAUNCH(true, false);
+        if (sw) MVX_MERGE_LAUNCH(true, true, false);
+        else MVX_MERGE_LAUNCH(true, false, false);
     }
 #undef MVX_MERGE_LAUNCH
     return hipGetLastError() == hipSuccess ? MPI_SUCCESS : MPI_ERR_OTHER;
