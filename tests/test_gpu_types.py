@@ -11,6 +11,8 @@
   oracle's replay -- whole recv buffers compared, so bytes outside the type
   map must keep the caller's pattern as in the reference.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -414,7 +416,7 @@ def _random_type(mvx, oracle, rng):
     return h, made
 
 
-@pytest.mark.parametrize("batch", range(8))
+@pytest.mark.parametrize("batch", range(int(os.environ.get("MVX_FUZZ_TYPEMAP_BATCHES", "8"))))
 def test_random_type_maps_pack_unpack(mvx, oracle, batch):
     """Seeded random type maps (_random_type) through every pack / unpack
     kernel the dispatch picks -- the tiled pack and whole-word unpack
