@@ -128,6 +128,7 @@ static long g_nt_min_bytes = 64L << 20;
 static int g_prog4 = 1;          // programs over 3-4 leaves on the KMAX = 4 kernels
 static int g_prog_u = 1;
 static int g_generic_only = 0;   // MVX_PROG_GENERIC=1: no fixed-tree kernels (A/B runs)
+static int g_chain_rt = 1;       // MVX_CHAIN_RT=0: chains of 5-7 leaves on the masked program (A/B)
 // resident blocks per CU for the non-temporal launches of each family (0 =
 // as many as registers allow); MVX_CAP_{APPLY,PROG,TREE} override for A/B runs
 static int g_cap[FAM_N] = {0, 0, 2};
@@ -187,6 +188,8 @@ static void init_env()
     if (e && atoi(e) == 1) g_generic_only = 1;
     e = getenv("MVX_PROG4");
     if (e && atoi(e) == 0) g_prog4 = 0;
+    e = getenv("MVX_CHAIN_RT");
+    if (e && atoi(e) == 0) g_chain_rt = 0;
     e = getenv("MVX_NO_BODY");
     if (e && atoi(e) == 1) g_no_body = 1;
     const char *caps[FAM_N] = {"MVX_CAP_APPLY", "MVX_CAP_PROG", "MVX_CAP_TREE"};
@@ -227,13 +230,15 @@ static int launch(const KSet *ks, const KFam &F, Params &P, hipStream_t stream)
     }
     bool folded = false;
     for (int q = 0; q < P.k; ++q) folded |= P.fold[q] != nullptr;
-    if (nt && F.body && !g_no_body && P.k == F.body_k && P.vec_ok && P.head == 0 && P.nvec > 0 &&
+    const bool body_k = P.k == F.body_k || (F.body_kmin && P.k >= F.body_kmin && P.k <= F.body_k);
+    if (nt && F.body && !g_no_body && body_k && P.vec_ok && P.head == 0 && P.nvec > 0 &&
         P.nvec * ks->chunk == P.n * es && !folded) {
         BodyParams B;
         memset(&B, 0, sizeof B);
         for (int q = 0; q < P.k; ++q) B.src[q] = reinterpret_cast<const u32x4 *>(P.src[q]);
         B.dst = reinterpret_cast<u32x4 *>(P.dst);
         B.nvec = P.nvec;
+        B.k = P.k;
         long work = (P.nvec * F.body_units + F.body_unroll * 256 - 1) / (F.body_unroll * 256);
         const unsigned blocks = (unsigned)(work < g_block_cap ? work : g_block_cap);
         void *bargs[] = {&B};
@@ -332,8 +337,11 @@ extern "C" int mvx_op_program(int op, int dtype, const void *const *srcs,
     for (int q = 0; q < k; ++q) folded |= P.fold[q] != nullptr;
     if (!g_generic_only && !folded && chain_mask == 0 && (k == 8 || k == 4) && tree_mask == mvx_tree_mask(k))
         return launch(ks, k == 8 ? ks->tree8 : ks->tree4, P, (hipStream_t)stream);
-    if (!g_generic_only && !folded && tree_mask == 0 && (k == 8 || k == 4) && chain_mask == mvx_chain_mask(k))
-        return launch(ks, k == 8 ? ks->chain8 : ks->chain4, P, (hipStream_t)stream);
+    /* chains of 5-7 leaves (pairwise Reduce_scatter at p = 5..7): the 8-leaf
+     * chain body with a run-time leaf count, else its masked program */
+    if (!g_generic_only && !folded && tree_mask == 0 && k >= 4 && chain_mask == mvx_chain_mask(k) &&
+        (k == 4 || g_chain_rt || k == 8))
+        return launch(ks, k == 4 ? ks->chain4 : ks->chain8, P, (hipStream_t)stream);
     if (g_prog_u == 2 && ks->prog2.fn[0])
         return launch(ks, ks->prog2, P, (hipStream_t)stream);
     if (k <= 4 && g_prog4)

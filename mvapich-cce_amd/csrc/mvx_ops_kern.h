@@ -541,6 +541,7 @@ struct BodyParams {
     const u32x4 *src[8];
     u32x4 *dst;
     long nvec;   // chunks
+    int k;       // leaves (k_chain_body<..., 8, ...>: 5 to 8)
 };
 
 // 56 KiB of static LDS per block: 2 resident blocks (8 waves) per CU.
@@ -587,13 +588,17 @@ k_tree_body(const BodyParams P)
 }
 
 // The same over a full CHAIN ((y0 op y1) op y2) ..., the pairwise
-// Reduce_scatter's order (C4: k = 4, p = 4)
+// Reduce_scatter's order (C4: k = 4, p = 4).  The 8-leaf instantiation
+// takes chains of 5 to 8 leaves (P.k, a wave-uniform test per leaf): the
+// pairwise chains at p = 5, 6, 7, which otherwise run the masked program at
+// one chunk per lane.
 template <int O, typename T, int KMAX, int U>
 __global__ void __launch_bounds__(256)
 k_chain_body(const BodyParams P)
 {
     __shared__ char lds_cap[BODY_LDS_CAP];
     if (P.nvec < 0) lds_cap[threadIdx.x] = 0;
+    const int k = KMAX == 8 ? P.k : KMAX;
     const long nthr = (long)gridDim.x * 256;
     for (long c0 = (long)blockIdx.x * (256 * U) + threadIdx.x; c0 < P.nvec; c0 += nthr * U) {
         Chunk<T> x[U][KMAX];
@@ -602,7 +607,8 @@ k_chain_body(const BodyParams P)
             const long c = c0 + (long)u * 256;
             if (c < P.nvec)
 #pragma unroll
-                for (int q = 0; q < KMAX; ++q) x[u][q] = ld_chunk<T, 1>(P.src[q], c);
+                for (int q = 0; q < KMAX; ++q)
+                    if (q < k) x[u][q] = ld_chunk<T, 1>(P.src[q], c);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -610,7 +616,7 @@ k_chain_body(const BodyParams P)
             if (c < P.nvec) {
 #pragma unroll
                 for (int q = 1; q < KMAX; ++q)
-                    CF<O, T>::f(x[u][0], x[u][q]);
+                    if (q < k) CF<O, T>::f(x[u][0], x[u][q]);
                 st_chunk<T, BODY_ST_NT>(P.dst, c, x[u][0]);
             }
         }
@@ -758,6 +764,7 @@ struct KFam {
     SymFn body_sym;
     int body_unroll;
     int body_k;            // the body kernel's leaf count (launches with other k never use it)
+    int body_kmin;         // or, when set, the fewest leaves it takes (k_chain_body<..., 8, ...>: 5)
     int body_units;        // 16-byte units one body thread moves per element (k_pxi_loc_body: 2)
     int body_cap;          // resident blocks per CU by a dynamic LDS reservation (0: none)
 };
@@ -801,6 +808,7 @@ static KFam kfam(int fam)
     f.fam = (fam == FAM_TREE && alu_heavy<T>::v) ? FAM_PROG : fam;
     f.body_units = 1;
     f.body_cap = 0;
+    f.body_kmin = 0;
     if constexpr (PROG == 1 && !alu_heavy<T>::v) {
         f.body = (const void *)&k_tree_body<O, T, KMAX, U1>;
         f.body_sym = &ksym_body<O, T, KMAX, U1>;
@@ -838,6 +846,7 @@ static KFam kchain()
         f.body_sym = &ksym_chain_body<O, T, KMAX, 2>;
         f.body_unroll = 2;
         f.body_k = KMAX;
+        f.body_kmin = KMAX == 8 ? 5 : 0;
     }
     return f;
 }

@@ -169,3 +169,24 @@ def test_three_leaf_programs_on_four_leaf_kernel(mvx, op, dtype, shape, folded):
         sym, got, ref = _run(mvx, op, dtype, k, shape, n, folded=folded)
         assert sym.startswith("k_combine<") and ", 4, 2, 1, 0>" in sym, sym
         assert np.array_equal(got, ref)
+
+
+@pytest.mark.parametrize("k", [5, 6, 7])
+@pytest.mark.parametrize("op,dtype", [(102, 10), (111, 17), (105, 8), (100, 11), (103, 11)])
+def test_five_to_seven_leaf_chains_on_the_eight_leaf_body(mvx, op, dtype, k):
+    """Chains of 5-7 leaves (the pairwise Reduce_scatter at p = 5..7) run the
+    8-leaf chain body with a run-time leaf count (k_chain_body<..., 8, 2>,
+    P.k) where the launch is large and aligned, and its masked program
+    otherwise -- bit for bit against the CPU replay either way; trees of 5-7
+    leaves keep the masked program."""
+    E = mvx.dtype_info(dtype)[0]
+    n = NT_ELEMS * 4 // E
+    sym, got, ref = _run(mvx, op, dtype, k, SHAPE_CHAIN, n, seed=k)
+    assert sym.startswith("k_chain_body<") and ", 8, 2>" in sym, sym
+    assert np.array_equal(got, ref)
+    sym, got, ref = _run(mvx, op, dtype, k, SHAPE_CHAIN, n, offset=4 if E == 4 else 8, seed=k + 1)
+    assert sym.startswith("k_combine<"), sym
+    assert np.array_equal(got, ref)
+    sym, got, ref = _run(mvx, op, dtype, k, SHAPE_TREE, n, seed=k + 2)
+    assert sym.startswith("k_combine<"), sym
+    assert np.array_equal(got, ref)
