@@ -277,3 +277,24 @@ def test_c5_full_size_allreduce_maxloc_float_int_8x64mi(mvx, oracle, comms, dist
     choices: loc = rank (3, every tie is settled by the min-loc rule across
     ranks) and loc = rank*n + i (4)."""
     _full_size(mvx, oracle, comms, "ar", 8, 64 << 20, 17, 111, dist)
+
+
+@pytest.mark.parametrize("p", [5, 6, 7])
+@pytest.mark.parametrize("op,dtype", [(102, 10), (105, 8)])
+def test_large_pairwise_reduce_scatter_five_to_seven_ranks(mvx, oracle, comms, p, op, dtype):
+    """The pairwise Reduce_scatter at p = 5..7 with blocks large enough for a
+    non-temporal combine: each rank's p-leaf chain runs the 8-leaf chain
+    body with a run-time leaf count (k_chain_body, MVX_CHAIN_RT) -- against
+    the reference schedule's replay."""
+    E = 4 if dtype == 10 else 8
+    blk = (16 << 20) // E
+    cnts = [blk] * p
+    sends = [T.rand_vec(dtype, blk * p, 4242 + 13 * p + r) for r in range(p)]
+    got, rcs = _run(mvx, comms[p], "rs", p, sends, cnts, dtype, op)
+    assert mvx.last_kernel_symbol().startswith("k_chain_body<"), mvx.last_kernel_symbol()
+    refs = [np.zeros(c, sends[0].dtype) for c in cnts]
+    rref = oracle.reduce_scatter([s.view(np.uint8) for s in sends], [x.view(np.uint8) for x in refs], cnts,
+                                 dtype, op)
+    assert rcs == rref
+    for r in range(p):
+        T.assert_same(op, dtype, got[r][: cnts[r] * E], refs[r], typemap_only=True)
